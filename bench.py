@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 3D poses/s of the 243-frame-RF, 17-joint, 1024-channel
+TemporalModelOptimized1f lifter on MI355X (BASELINE.json config 2; config 4
+when launched with N > 1 ranks: the window batch is sharded, no collective).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16]
+
+One step = one eval-mode forward of B independent 243-frame windows that are
+already resident in HBM (B poses out).  Every rank processes its own B windows
+(weak scaling); `value` = N*B*K / max-over-ranks(wall time of K steps).
+
+Besides the JSON contract fields the line carries
+  roofline      dominant kernel (block-1 k3 conv GEMM) FLOP per launch / its average
+                HIP-event duration on the launch stream during the timed steps
+  cpu_baseline  the oracle (the reference's torch-CPU op sequence) on this host
+  parity        MPJPE delta vs the oracle on a window subset, fp32 and the timed dtype
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "dynamic-camera-augmented-videopose3d_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "3D poses/sec, 243-frame RF, 17 joints, 1024ch; MPJPE vs ref"
+FW = [3, 3, 3, 3, 3]
+CHANNELS = 1024
+JOINTS = 17
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8192, help="windows per GPU per step")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--traj", action="store_true",
+                    help="config 3: camera-trajectory conditioned input (46 ch) with the "
+                         "on-device window gather inside the timed step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="approximate CPU-baseline sample duration (0 disables)")
+    ap.add_argument("--parity-windows", type=int, default=32)
+    return ap.parse_args()
+
+
+def synth_windows(B, T, jin, seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    base = (torch.rand((B, 1, jin, 2), generator=g, device=device) - 0.5) * 1.2
+    steps = torch.randn((B, T, jin, 2), generator=g, device=device) * 0.003
+    return (base + torch.cumsum(steps, dim=1)).contiguous()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from common.models.TemporalModel import TemporalModelOptimized1f
+    from vp3d_amd import synth
+
+    jin = 23 if args.traj else JOINTS
+    model = TemporalModelOptimized1f(jin, 2, JOINTS, FW, channels=CHANNELS)
+    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.eval().cuda()
+    model.set_compute_dtype(args.dtype)
+    RF = model.receptive_field()
+    B = args.batch
+
+    pipe = None
+    if args.traj:
+        from vp3d_amd.pipeline import SyntheticTrajectoryBatcher
+        pipe = SyntheticTrajectoryBatcher(B, RF, seed=1000 + rank, device=dev)
+        x = pipe.next_batch()
+    else:
+        x = synth_windows(B, RF, jin, 1000 + rank, dev)
+    lifter = model.native_lifter(dev)
+    lifter.reserve(B, RF, args.dtype)
+    y = torch.empty((B, 1, JOINTS, 3), device=dev)
+
+    def step():
+        xin = pipe.next_batch() if pipe is not None else x
+        lifter.forward(xin, args.dtype, out=y)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        lifter.profile(True)
+        lifter.profile_reset()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        lifter.profile(False)
+    prof = lifter.profile_read()
+
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    total_poses = world * B * args.steps
+    value = total_poses / dt
+    # dominant kernel: largest accumulated time
+    dom = max(prof, key=lambda r: r["ms_total"])
+    dom_avg_ms = dom["ms_total"] / max(dom["launches"], 1)
+    achieved = dom["flop"] / (dom_avg_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    layer_names = ["expand"] + [f"block{(i // 2) + 1}_{'k3' if i % 2 == 0 else '1x1'}"
+                                for i in range(2 * (len(FW) - 1))] + ["shrink"]
+    per_layer = {layer_names[r["layer"]]: round(r["ms_total"] / max(r["launches"], 1), 4)
+                 for r in prof}
+
+    out = None
+    if rank == 0:
+        # ---- parity on a window subset (oracle = reference op sequence on CPU) ----
+        from oracle.temporal_ref import lifter_forward
+        P = min(args.parity_windows, B)
+        xs = (pipe.next_batch() if pipe is not None else x)[:P].contiguous()
+        with torch.no_grad():
+            y_fast = model(xs).cpu().numpy()
+            model.set_compute_dtype("fp32")
+            y_32 = model(xs).cpu().numpy()
+            model.set_compute_dtype(args.dtype)
+        ref = lifter_forward(sd, xs.cpu(), FW, strided=True).numpy()
+        gt = synth.gt_poses(3, "bench_gt", P, JOINTS).reshape(ref.shape)
+
+        def mp(a):
+            return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
+        parity = {
+            "windows": P,
+            "mpjpe_ref_mm": round(mp(ref) * 1e3, 6),
+            "fp32_mpjpe_delta_mm": abs(mp(y_32) - mp(ref)) * 1e3,
+            "fp32_max_coord_delta_mm": float(np.abs(y_32 - ref).max()) * 1e3,
+            f"{args.dtype}_mpjpe_delta_mm": abs(mp(y_fast) - mp(ref)) * 1e3,
+            f"{args.dtype}_max_coord_delta_mm": float(np.abs(y_fast - ref).max()) * 1e3,
+        }
+
+        # ---- CPU baseline: the oracle on a bounded sample of the same workload ----
+        cpu = None
+        if args.cpu_seconds > 0:
+            nthr = torch.get_num_threads()
+            cb = 64
+            xc = xs[:1].cpu().expand(cb, -1, -1, -1).contiguous()
+            lifter_forward(sd, xc[:8], FW, strided=True)  # warm-up
+            n, t_cpu = 0, 0.0
+            while t_cpu < args.cpu_seconds:
+                t1 = time.perf_counter()
+                lifter_forward(sd, xc, FW, strided=True)
+                t_cpu += time.perf_counter() - t1
+                n += cb
+            cpu = {"value": round(n / t_cpu, 2), "unit": "poses/s", "cores": nthr, "kind": "port",
+                   "sample": f"{n} windows of 243x17x2 through the torch-CPU restatement "
+                             f"(oracle/temporal_ref.py, fp32, batch {cb}) in {t_cpu:.1f} s"}
+
+        traffic = None
+        tfile = os.path.join(REPO, "profiles", f"traffic_{args.dtype}_b{B}.json")
+        if os.path.exists(tfile):
+            with open(tfile) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+
+        flop_pose = 358541312 if args.traj else 352569344
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "poses/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded random-walk 2D windows, counter-hash weights)",
+            "config": {
+                "workload": ("config3 trajectory-conditioned (46ch) " if args.traj else "config2 ")
+                            + "TemporalModelOptimized1f 243-frame RF windows, 17 joints, 1024 ch",
+                "windows_per_gpu": B,
+                "global_batch": B * world,
+                "parallelism": f"dp{world} (independent window shards, no collective)",
+                "flop_per_pose": flop_pose,
+            },
+            "tflops_effective": round(value * flop_pose / 1e12, 2),
+            "roofline": {
+                "bound": "mfma",
+                "kernel": f"conv_gemm ({layer_names[dom['layer']]})",
+                "achieved": round(achieved, 2),
+                "peak": peak,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4),
+                "traffic": traffic,
+                "avg_launch_ms": round(dom_avg_ms, 4),
+                "flop_per_launch": dom["flop"],
+            },
+            "per_layer_ms": per_layer,
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        if cpu:
+            out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,64 @@
+// Internal launch interface between the C-ABI (vp3d_capi.cpp) and the HIP
+// kernels.  Not part of the public boundary (include/vp3d.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vp3d {
+
+// One temporal convolution layer of the lifter expressed as a GEMM over rows
+// (b, t) of channel-last activations:
+//
+//   Y[m, n] = epi( sum_{tap, c} X[src(m) + tap*dil, c] * W[n, tap*Ktap + c] )
+//   src(m)  = (m / T_out) * T_in + (m % T_out) * stride
+//   epi(v)  = [relu](v * scale[n] + shift[n]) [+ R[res(m), n]]
+//   res(m)  = (m / T_out) * R_T + (m % T_out) * R_stride + R_off
+//
+// This covers every convolution in TemporalModel.py:
+//   expand_conv (dilated variant)  stride 1,  taps contiguous (one tap of 3*Cin)
+//   expand_conv (Optimized1f)      stride w0, taps contiguous
+//   layers_conv[2i] (dilated)      stride 1,  3 taps at row offsets {0, d, 2d}
+//   layers_conv[2i] (Optimized1f)  stride w,  taps contiguous
+//   layers_conv[2i+1] (1x1)        + residual slice (TemporalModel.py:132,192)
+//   shrink (1x1 + bias)            scale = 1, shift = bias, no relu
+struct ConvGemmParams {
+    const void* A;       // activations: f32 or bf16/f16 rows of `lda` elements
+    const void* W;       // packed weights [Np][Kp] (f32 or bf16/f16), zero padded
+    const float* scale;  // [N]
+    const float* shift;  // [N]
+    const void* R;       // residual rows (output dtype) or nullptr
+    void* Y;             // output rows of `ldy` elements
+    int M, N, K, Kp;
+    int T_out, T_in, stride, dil, Ktap, lda;
+    int R_T, R_stride, R_off, ldr;
+    int ldy;
+    int relu;
+};
+
+enum class Act { F32 = 0, BF16 = 1, F16 = 2 };
+
+// A: element type of the activation input; Y/R: element type of the output.
+// compute: F32 -> exact f32 MFMA; BF16/F16 -> 16-bit MFMA with f32 accumulate
+// (weights in the same 16-bit type).
+hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, Act compute,
+                            hipStream_t stream);
+
+// Tile geometry the packer must pad to.
+constexpr int kPadN = 128;
+constexpr int kPadK = 64;
+
+// preprocess kernels (preprocess.hip)
+hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, float* out,
+                                   bool inverse, hipStream_t s);
+hipError_t launch_camera_matrices(const float* intr, const int32_t* frame_seq, const double* extr,
+                                  int64_t n_frames, float* out, hipStream_t s);
+hipError_t launch_world_to_camera(const float* X, int64_t n, const float q[4], const float t[3],
+                                  float* out, hipStream_t s);
+hipError_t launch_gather_windows(const float* kps, int f2, const float* cams,
+                                 const int64_t* seq_off, const int32_t* seq_len,
+                                 const int32_t* pairs, int B, int window, int pad, int shift,
+                                 float* out, hipStream_t s);
+hipError_t launch_mpjpe_accumulate(const float* pred, const float* target, int64_t n,
+                                   double* acc, hipStream_t s);
+
+}  // namespace vp3d

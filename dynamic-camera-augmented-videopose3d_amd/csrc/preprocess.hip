@@ -1,0 +1,198 @@
+// On-device input path of the lifter (HBM-bound element/gather kernels).
+//
+//   normalize_screen   reference common/camera.py:14-18 (+ inverse, :21-25)
+//   camera_matrices    reference common/generators.py:115-125, :180-190 (K @ E_t)
+//   world_to_camera    reference common/camera.py:28-30, common/quaternion.py:10-35
+//   gather_windows     reference common/generators.py:92-137 (pad_chunk, 'edge'),
+//                      :193-198, fused with the trajectory concat of
+//                      common/models/CamTransformer.py:187-190
+//   mpjpe_accumulate   reference common/loss.py:11-17
+//
+// None of these contract multiply-adds: the reference evaluates them with
+// separately rounded numpy / torch-CPU operations, and the kernels reproduce that
+// rounding sequence (explicit _rn intrinsics) so integer-exact parity holds where
+// the reference's own arithmetic is order-independent.
+#include "kernels.h"
+
+namespace vp3d {
+namespace {
+
+constexpr int kThreads = 256;
+
+inline dim3 grid_for(int64_t n, int per_thread = 1) {
+    int64_t blocks = (n + (int64_t)kThreads * per_thread - 1) / ((int64_t)kThreads * per_thread);
+    if (blocks < 1) blocks = 1;
+    if (blocks > 65535 * 16) blocks = 65535 * 16;
+    return dim3((unsigned)blocks);
+}
+
+// X/w*2 - [1, h/w]: numpy evaluates X/w and *2 in float32 (array op with a
+// Python int), then subtracts a float64 list, i.e. in float64, and run.py
+// stores the float64 result back into a float32 array (one final rounding).
+__global__ void normalize_screen_kernel(const float* __restrict__ x, int64_t n, float wf,
+                                        double hw, float* __restrict__ out, int inverse,
+                                        float halfw) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float2 v = reinterpret_cast<const float2*>(x)[i];
+        float2 r;
+        if (!inverse) {
+            const float a = __fmul_rn(__fdiv_rn(v.x, wf), 2.0f);
+            const float b = __fmul_rn(__fdiv_rn(v.y, wf), 2.0f);
+            r.x = (float)__dsub_rn((double)a, 1.0);
+            r.y = (float)__dsub_rn((double)b, hw);
+        } else {
+            // (X + [1, h/w]) * w / 2: float64 add (list promotion), then *w and /2 in float64
+            r.x = (float)__ddiv_rn(__dmul_rn(__dadd_rn((double)v.x, 1.0), (double)wf), 2.0);
+            r.y = (float)__ddiv_rn(__dmul_rn(__dadd_rn((double)v.y, hw), (double)wf), 2.0);
+        }
+        reinterpret_cast<float2*>(out)[i] = r;
+        (void)halfw;
+    }
+}
+
+// K (float32, from the sequence's intrinsics) @ E_t (float64) in float64,
+// rounded once to float32 when run.py casts the batch (`astype('float32')`).
+// K = [[fx,0,cx],[0,fy,cy],[0,0,1]] so each entry has at most two non-zero
+// products; their sum is order-independent, hence bit-exact.
+__global__ void camera_matrices_kernel(const float* __restrict__ intr,
+                                       const int32_t* __restrict__ frame_seq,
+                                       const double* __restrict__ extr, int64_t n,
+                                       float* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n * 12;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t f = i / 12;
+        const int e = (int)(i - f * 12);
+        const int row = e >> 2, col = e & 3;
+        const float* K = intr + 4 * (int64_t)frame_seq[f];
+        const double* E = extr + 12 * f;
+        double v;
+        if (row == 0)
+            v = __dadd_rn(__dmul_rn((double)K[0], E[col]), __dmul_rn((double)K[2], E[8 + col]));
+        else if (row == 1)
+            v = __dadd_rn(__dmul_rn((double)K[1], E[4 + col]), __dmul_rn((double)K[3], E[8 + col]));
+        else
+            v = E[8 + col];
+        out[i] = (float)v;
+    }
+}
+
+// qrot(q, v) = v + 2 * (w * (q_xyz x v) + q_xyz x (q_xyz x v)), q = qinverse(R).
+__global__ void world_to_camera_kernel(const float* __restrict__ X, int64_t n, float qw,
+                                       float qx, float qy, float qz, float tx, float ty,
+                                       float tz, float* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float vx = __fsub_rn(X[3 * i + 0], tx);
+        const float vy = __fsub_rn(X[3 * i + 1], ty);
+        const float vz = __fsub_rn(X[3 * i + 2], tz);
+        // uv = cross(qvec, v)
+        const float uvx = __fsub_rn(__fmul_rn(qy, vz), __fmul_rn(qz, vy));
+        const float uvy = __fsub_rn(__fmul_rn(qz, vx), __fmul_rn(qx, vz));
+        const float uvz = __fsub_rn(__fmul_rn(qx, vy), __fmul_rn(qy, vx));
+        // uuv = cross(qvec, uv)
+        const float uuvx = __fsub_rn(__fmul_rn(qy, uvz), __fmul_rn(qz, uvy));
+        const float uuvy = __fsub_rn(__fmul_rn(qz, uvx), __fmul_rn(qx, uvz));
+        const float uuvz = __fsub_rn(__fmul_rn(qx, uvy), __fmul_rn(qy, uvx));
+        out[3 * i + 0] = __fadd_rn(vx, __fmul_rn(2.f, __fadd_rn(__fmul_rn(qw, uvx), uuvx)));
+        out[3 * i + 1] = __fadd_rn(vy, __fmul_rn(2.f, __fadd_rn(__fmul_rn(qw, uvy), uuvy)));
+        out[3 * i + 2] = __fadd_rn(vz, __fmul_rn(2.f, __fadd_rn(__fmul_rn(qw, uvz), uuvz)));
+    }
+}
+
+// One thread per output element (b, t, c) of the (B, window, F2 [+12]) window
+// tensor; consecutive threads walk c, so reads of one frame's keypoints and
+// writes of one window row are contiguous.
+__global__ void gather_windows_kernel(const float* __restrict__ kps, int f2,
+                                      const float* __restrict__ cams,
+                                      const int64_t* __restrict__ seq_off,
+                                      const int32_t* __restrict__ seq_len,
+                                      const int32_t* __restrict__ pairs, int B, int window,
+                                      int lead, float* __restrict__ out) {
+    const int fo = f2 + (cams ? 12 : 0);
+    const int64_t total = (int64_t)B * window * fo;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t bt = i / fo;
+        const int c = (int)(i - bt * fo);
+        const int b = (int)(bt / window);
+        const int t = (int)(bt - (int64_t)b * window);
+        const int seq = pairs[2 * b];
+        const int len = seq_len[seq];
+        int f = pairs[2 * b + 1] - lead + t;
+        f = f < 0 ? 0 : (f >= len ? len - 1 : f);
+        const int64_t frame = seq_off[seq] + f;
+        out[i] = (c < f2) ? kps[frame * f2 + c] : cams[frame * 12 + (c - f2)];
+    }
+}
+
+// Block-reduced sum of per-joint Euclidean distances in float64.
+__global__ void mpjpe_kernel(const float* __restrict__ pred, const float* __restrict__ target,
+                             int64_t n, double* __restrict__ acc) {
+    double s = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float dx = pred[3 * i] - target[3 * i];
+        const float dy = pred[3 * i + 1] - target[3 * i + 1];
+        const float dz = pred[3 * i + 2] - target[3 * i + 2];
+        s += sqrt((double)dx * dx + (double)dy * dy + (double)dz * dz);
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    __shared__ double part[kThreads / 64];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < kThreads / 64; ++w) t += part[w];
+        atomicAdd(acc, t);
+        if (blockIdx.x == 0) atomicAdd(acc + 1, (double)n);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, float* out,
+                                   bool inverse, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const double hw = (double)h / (double)w;
+    hipLaunchKernelGGL(normalize_screen_kernel, grid_for(n, 4), dim3(kThreads), 0, s, x, n,
+                       (float)w, hw, out, inverse ? 1 : 0, 0.f);
+    return hipGetLastError();
+}
+
+hipError_t launch_camera_matrices(const float* intr, const int32_t* frame_seq, const double* extr,
+                                  int64_t n_frames, float* out, hipStream_t s) {
+    if (n_frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(camera_matrices_kernel, grid_for(n_frames * 12, 4), dim3(kThreads), 0, s,
+                       intr, frame_seq, extr, n_frames, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_world_to_camera(const float* X, int64_t n, const float q[4], const float t[3],
+                                  float* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    // qinverse (quaternion.py:27-35): (w, -x, -y, -z)
+    hipLaunchKernelGGL(world_to_camera_kernel, grid_for(n, 4), dim3(kThreads), 0, s, X, n, q[0],
+                       -q[1], -q[2], -q[3], t[0], t[1], t[2], out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_windows(const float* kps, int f2, const float* cams,
+                                 const int64_t* seq_off, const int32_t* seq_len,
+                                 const int32_t* pairs, int B, int window, int pad, int shift,
+                                 float* out, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    const int64_t total = (int64_t)B * window * (f2 + (cams ? 12 : 0));
+    hipLaunchKernelGGL(gather_windows_kernel, grid_for(total, 4), dim3(kThreads), 0, s, kps, f2,
+                       cams, seq_off, seq_len, pairs, B, window, pad + shift, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_mpjpe_accumulate(const float* pred, const float* target, int64_t n,
+                                   double* acc, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mpjpe_kernel, grid_for(n, 8), dim3(kThreads), 0, s, pred, target, n, acc);
+    return hipGetLastError();
+}
+
+}  // namespace vp3d

@@ -1,0 +1,626 @@
+// C-ABI of the MI355X-native temporal lifter (declared in include/vp3d.h).
+//
+// Host-side responsibilities, each mirroring a piece of the reference:
+//   * configuration and shape rules  — TemporalModel.py:15-33, 85-124, 152-186
+//     (pad / causal_shift / dilation bookkeeping, receptive_field :40-47,
+//      total_causal_shift :49-60 incl. quirk Q5)
+//   * weight folding and packing     — eval BatchNorm1d (TemporalModel.py:32,117,119)
+//     folded to per-channel scale/shift exactly as ATen's CPU batch_norm does
+//     (alpha = weight * 1/sqrt(var + eps), beta = bias - mean * alpha); conv
+//     weights (Cout, Cin, k) packed tap-major [Cout][k*Cin] for the GEMM kernels
+//   * forward orchestration          — TemporalModel._forward_blocks :126-138 and
+//     TemporalModelOptimized1f._forward_blocks :188-198, one GEMM launch per conv
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vp3d.h"
+#include "kernels.h"
+
+using namespace vp3d;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return fail(_e == hipErrorOutOfMemory ? VP3D_ERR_OOM : VP3D_ERR_HIP,         \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));             \
+    } while (0)
+
+uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+uint16_t f32_to_f16_rne(float f) {
+    _Float16 h = (_Float16)f;
+    uint16_t r;
+    std::memcpy(&r, &h, 2);
+    return r;
+}
+
+struct Layer {
+    int cin = 0, cout = 0, taps = 1, dil = 1, stride = 1;  // conv geometry
+    int K = 0, Kp = 0, Np = 0, Ktap = 0, gemm_taps = 1;     // GEMM geometry
+    bool relu = true;
+    bool residual = false;  // 1x1 conv of a block: add the block-input slice
+    int res_stride = 1, res_off = 0;
+    float* w32 = nullptr;
+    uint16_t* wbf = nullptr;
+    uint16_t* wh = nullptr;
+    float* scale = nullptr;
+    float* shift = nullptr;
+};
+
+struct ProfEvent {
+    int layer;
+    hipEvent_t a, b;
+    double flop;
+};
+
+}  // namespace
+
+struct vp3d_handle {
+    vp3d_cfg cfg{};
+    int device = 0;
+    std::vector<int> pad, causal_shift;
+    std::vector<Layer> layers;  // expand, (conv_k, conv_1x1) per block, shrink
+    // activation workspace: three buffers of ws_elems elements of ws_esize bytes
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    // profiling
+    bool profiling = false;
+    std::vector<ProfEvent> pending;
+    std::vector<hipEvent_t> free_events;
+    std::vector<double> prof_ms;
+    std::vector<int64_t> prof_n;
+    std::vector<double> prof_flop;
+};
+
+namespace {
+
+int validate_cfg(const vp3d_cfg* c) {
+    if (!c) return fail(VP3D_ERR_ARG, "cfg is NULL");
+    if (c->n_widths < 1 || c->n_widths > VP3D_MAX_BLOCKS)
+        return fail(VP3D_ERR_ASSERT, "filter_widths must have 1..8 entries");
+    for (int i = 0; i < c->n_widths; ++i)
+        if (c->filter_widths[i] <= 0 || c->filter_widths[i] % 2 == 0)
+            return fail(VP3D_ERR_ASSERT, "Only odd filter widths are supported");  // TemporalModel.py:21
+    if (c->num_joints_in <= 0 || c->in_features <= 0 || c->num_joints_out <= 0 || c->channels <= 0)
+        return fail(VP3D_ERR_ASSERT, "joint/feature/channel counts must be positive");
+    if (c->variant != VP3D_VARIANT_DILATED && c->variant != VP3D_VARIANT_STRIDED_1F)
+        return fail(VP3D_ERR_ARG, "unknown variant");
+    if (c->variant == VP3D_VARIANT_STRIDED_1F && c->dense)
+        return fail(VP3D_ERR_ARG, "TemporalModelOptimized1f has no dense option");
+    if (c->channels % 8 != 0)
+        return fail(VP3D_ERR_ARG, "channels must be a multiple of 8 for the MFMA kernels");
+    return VP3D_OK;
+}
+
+// pad / causal_shift bookkeeping (TemporalModel.py:31,107-111 and :173-177)
+void build_geometry(vp3d_handle* h) {
+    const vp3d_cfg& c = h->cfg;
+    const int* fw = c.filter_widths;
+    const bool f1 = c.variant == VP3D_VARIANT_STRIDED_1F;
+    h->pad.assign(1, fw[0] / 2);
+    h->causal_shift.assign(1, c.causal ? fw[0] / 2 : 0);
+    const int C = c.channels;
+    const int cin0 = c.num_joints_in * c.in_features;
+
+    h->layers.clear();
+    Layer ex;
+    ex.cin = cin0;
+    ex.cout = C;
+    ex.taps = fw[0];
+    ex.dil = 1;
+    ex.stride = f1 ? fw[0] : 1;
+    h->layers.push_back(ex);
+
+    int next_dilation = fw[0];
+    for (int i = 1; i < c.n_widths; ++i) {
+        const int w = fw[i];
+        const int pad_i = (w - 1) * next_dilation / 2;
+        h->pad.push_back(pad_i);
+        if (f1)
+            h->causal_shift.push_back(c.causal ? w / 2 : 0);
+        else
+            h->causal_shift.push_back(c.causal ? (w / 2) * next_dilation : 0);
+
+        Layer kc;
+        kc.cin = C;
+        kc.cout = C;
+        if (f1) {
+            kc.taps = w;
+            kc.dil = 1;
+            kc.stride = w;
+        } else if (c.dense) {
+            kc.taps = 2 * pad_i + 1;
+            kc.dil = 1;
+            kc.stride = 1;
+        } else {
+            kc.taps = w;
+            kc.dil = next_dilation;
+            kc.stride = 1;
+        }
+        h->layers.push_back(kc);
+
+        Layer pw;
+        pw.cin = C;
+        pw.cout = C;
+        pw.taps = 1;
+        pw.residual = true;
+        if (f1) {
+            pw.res_stride = w;
+            pw.res_off = h->causal_shift.back() + w / 2;  // TemporalModel.py:192
+        } else {
+            pw.res_stride = 1;
+            pw.res_off = pad_i + h->causal_shift.back();  // TemporalModel.py:132
+        }
+        h->layers.push_back(pw);
+        next_dilation *= w;
+    }
+    Layer sh;
+    sh.cin = C;
+    sh.cout = c.num_joints_out * 3;
+    sh.taps = 1;
+    sh.relu = false;
+    h->layers.push_back(sh);
+
+    for (Layer& L : h->layers) {
+        if (L.dil == 1) {  // taps are adjacent rows: one contiguous K segment
+            L.gemm_taps = 1;
+            L.Ktap = L.taps * L.cin;
+        } else {
+            L.gemm_taps = L.taps;
+            L.Ktap = L.cin;
+        }
+        L.K = L.taps * L.cin;
+        L.Kp = (L.K + kPadK - 1) / kPadK * kPadK;
+        L.Np = (L.cout + kPadN - 1) / kPadN * kPadN;
+    }
+}
+
+void free_layers(vp3d_handle* h) {
+    for (Layer& L : h->layers) {
+        hipFree(L.w32);
+        hipFree(L.wbf);
+        hipFree(L.wh);
+        hipFree(L.scale);
+        hipFree(L.shift);
+        L.w32 = nullptr;
+        L.wbf = L.wh = nullptr;
+        L.scale = L.shift = nullptr;
+    }
+}
+
+int upload_weights(vp3d_handle* h, const float* const* w, int n) {
+    const int expect = vp3d_weight_count(&h->cfg);
+    if (!w) return fail(VP3D_ERR_ARG, "weights is NULL");
+    if (n != expect)
+        return fail(VP3D_ERR_ARG, "expected " + std::to_string(expect) + " weight arrays, got " +
+                                      std::to_string(n));
+    for (int i = 0; i < n; ++i)
+        if (!w[i]) return fail(VP3D_ERR_ARG, "weight array " + std::to_string(i) + " is NULL");
+    const float eps = h->cfg.bn_eps;
+    const int nl = (int)h->layers.size();
+    int wi = 0;
+    for (int li = 0; li < nl; ++li) {
+        Layer& L = h->layers[li];
+        const bool is_shrink = li == nl - 1;
+        const float* cw = w[wi++];  // (cout, cin, taps)
+        std::vector<float> p32((size_t)L.Np * L.Kp, 0.f);
+        for (int o = 0; o < L.cout; ++o)
+            for (int c = 0; c < L.cin; ++c)
+                for (int k = 0; k < L.taps; ++k)
+                    p32[(size_t)o * L.Kp + (size_t)k * L.cin + c] =
+                        cw[((size_t)o * L.cin + c) * L.taps + k];
+        std::vector<float> sc(L.cout), shv(L.cout);
+        if (!is_shrink) {
+            const float* g = w[wi++];
+            const float* b = w[wi++];
+            const float* mu = w[wi++];
+            const float* var = w[wi++];
+            for (int o = 0; o < L.cout; ++o) {
+                const float invstd = 1.0f / std::sqrt(var[o] + eps);
+                sc[o] = invstd * g[o];
+                shv[o] = b[o] - mu[o] * sc[o];
+            }
+        } else {
+            const float* bias = w[wi++];
+            for (int o = 0; o < L.cout; ++o) {
+                sc[o] = 1.0f;
+                shv[o] = bias[o];
+            }
+        }
+        std::vector<uint16_t> pbf(p32.size()), ph(p32.size());
+        for (size_t i = 0; i < p32.size(); ++i) {
+            pbf[i] = f32_to_bf16_rne(p32[i]);
+            ph[i] = f32_to_f16_rne(p32[i]);
+        }
+        if (!L.w32) {
+            HIP_TRY(hipMalloc(&L.w32, p32.size() * 4));
+            HIP_TRY(hipMalloc(&L.wbf, p32.size() * 2));
+            HIP_TRY(hipMalloc(&L.wh, p32.size() * 2));
+            HIP_TRY(hipMalloc(&L.scale, L.cout * 4));
+            HIP_TRY(hipMalloc(&L.shift, L.cout * 4));
+        }
+        HIP_TRY(hipMemcpy(L.w32, p32.data(), p32.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(L.wbf, pbf.data(), pbf.size() * 2, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(L.wh, ph.data(), ph.size() * 2, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(L.scale, sc.data(), L.cout * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(L.shift, shv.data(), L.cout * 4, hipMemcpyHostToDevice));
+    }
+    return VP3D_OK;
+}
+
+// Temporal length after each layer for an input of T frames; returns false if
+// T is too short or the residual slice would not line up with the block output
+// (the reference raises in that case: a size-mismatched add).
+bool layer_lengths(const vp3d_handle* h, int T, std::vector<int>& len) {
+    len.clear();
+    int L = T;
+    for (const Layer& ly : h->layers) {
+        const int span = (ly.taps - 1) * ly.dil + 1;
+        if (L < span) return false;
+        const int out = (L - span) / ly.stride + 1;
+        if (ly.residual) {
+            // block input length is len[len.size()-2] (input of the k-conv)
+        }
+        len.push_back(out);
+        L = out;
+    }
+    // residual consistency: block b (1-based) input length = len[2b-2], output len[2b]
+    const int nb = h->cfg.n_widths - 1;
+    for (int b = 1; b <= nb; ++b) {
+        const Layer& pw = h->layers[2 * b];
+        const int lin = len[2 * b - 2];
+        const int lout = len[2 * b];
+        int rlen;
+        if (pw.res_stride == 1)
+            rlen = lin - 2 * h->pad[b];
+        else
+            rlen = (lin - pw.res_off + pw.res_stride - 1) / pw.res_stride;
+        if (rlen != lout) return false;
+    }
+    return true;
+}
+
+size_t esize(int dtype) { return dtype == VP3D_DTYPE_F32 ? 4 : 2; }
+
+int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
+    std::vector<int> len;
+    if (!layer_lengths(h, T, len)) return fail(VP3D_ERR_ARG, "input too short for the receptive field");
+    const size_t rows = (size_t)B * len[0];
+    const size_t need = 3 * rows * h->cfg.channels * esize(dtype);
+    if (need <= h->ws_bytes) return VP3D_OK;
+    if (h->ws) HIP_TRY(hipFree(h->ws));
+    h->ws = nullptr;
+    h->ws_bytes = 0;
+    HIP_TRY(hipMalloc(&h->ws, need));
+    h->ws_bytes = need;
+    return VP3D_OK;
+}
+
+hipEvent_t get_event(vp3d_handle* h) {
+    if (!h->free_events.empty()) {
+        hipEvent_t e = h->free_events.back();
+        h->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vp3d_abi_version(void) { return VP3D_ABI_VERSION; }
+
+const char* vp3d_last_error(void) { return g_last_error.c_str(); }
+
+int vp3d_weight_count(const vp3d_cfg* cfg) {
+    if (validate_cfg(cfg) != VP3D_OK) return -1;
+    return 5 + 10 * (cfg->n_widths - 1) + 2;
+}
+
+int vp3d_create(const vp3d_cfg* cfg, const float* const* weights, int n_weights, vp3d_handle** out) {
+    if (!out) return fail(VP3D_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int rc = validate_cfg(cfg);
+    if (rc) return rc;
+    vp3d_handle* h = new vp3d_handle();
+    h->cfg = *cfg;
+    if (h->cfg.bn_eps <= 0.f) h->cfg.bn_eps = 1e-5f;
+    hipGetDevice(&h->device);
+    build_geometry(h);
+    rc = upload_weights(h, weights, n_weights);
+    if (rc) {
+        free_layers(h);
+        delete h;
+        return rc;
+    }
+    h->prof_ms.assign(h->layers.size(), 0.0);
+    h->prof_n.assign(h->layers.size(), 0);
+    h->prof_flop.assign(h->layers.size(), 0.0);
+    *out = h;
+    return VP3D_OK;
+}
+
+int vp3d_load_weights(vp3d_handle* h, const float* const* weights, int n_weights) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev != h->device) return fail(VP3D_ERR_STATE, "handle belongs to another device");
+    return upload_weights(h, weights, n_weights);
+}
+
+int vp3d_destroy(vp3d_handle* h) {
+    if (!h) return VP3D_OK;
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(h->device);
+    free_layers(h);
+    if (h->ws) hipFree(h->ws);
+    for (auto& e : h->pending) {
+        hipEventDestroy(e.a);
+        hipEventDestroy(e.b);
+    }
+    for (auto e : h->free_events) hipEventDestroy(e);
+    hipSetDevice(prev);
+    delete h;
+    return VP3D_OK;
+}
+
+int vp3d_receptive_field(const vp3d_handle* h) {
+    if (!h) return -1;
+    int frames = 0;
+    for (int p : h->pad) frames += p;
+    return 1 + 2 * frames;
+}
+
+int vp3d_total_causal_shift(const vp3d_handle* h) {
+    // Bit-compatible with TemporalModel.py:49-60, including quirk Q5 (the
+    // dilated variant's causal_shift is already dilation-scaled and is scaled again).
+    if (!h) return -1;
+    int frames = h->causal_shift[0];
+    int next_dilation = h->cfg.filter_widths[0];
+    for (int i = 1; i < h->cfg.n_widths; ++i) {
+        frames += h->causal_shift[i] * next_dilation;
+        next_dilation *= h->cfg.filter_widths[i];
+    }
+    return frames;
+}
+
+int vp3d_out_frames(const vp3d_handle* h, int T) {
+    if (!h) return -1;
+    std::vector<int> len;
+    if (!layer_lengths(h, T, len)) return -1;
+    return len.back();
+}
+
+int vp3d_layer_count(const vp3d_handle* h) { return h ? (int)h->layers.size() : -1; }
+
+int vp3d_reserve(vp3d_handle* h, int B, int T, int dtype) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
+    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    return ensure_ws(h, B, T, dtype);
+}
+
+int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    if (!x || !y) return fail(VP3D_ERR_ARG, "x / y is NULL");
+    if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
+    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev != h->device) return fail(VP3D_ERR_STATE, "handle belongs to another device");
+    // Any T the reference's conv/slice length rules accept is accepted (for
+    // Optimized1f that is T == RF in practice); too-short inputs and
+    // residual/conv length mismatches fail like torch does (RuntimeError).
+    std::vector<int> len;
+    if (!layer_lengths(h, T, len))
+        return fail(VP3D_ERR_ARG, "input of " + std::to_string(T) +
+                                      " frames does not fit the receptive field of " +
+                                      std::to_string(vp3d_receptive_field(h)));
+    int rc = ensure_ws(h, B, T, dtype);
+    if (rc) return rc;
+
+    hipStream_t s = (hipStream_t)stream;
+    const Act act = dtype == VP3D_DTYPE_F32 ? Act::F32 : (dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16);
+    const size_t es = esize(dtype);
+    const size_t buf_elems = (size_t)B * len[0] * h->cfg.channels;
+    char* base = (char*)h->ws;
+    void* buf[3] = {base, base + buf_elems * es, base + 2 * buf_elems * es};
+
+    const int nl = (int)h->layers.size();
+    const void* cur_in = x;  // f32 input
+    int cur_len = T;
+    int xin_buf = -1;        // buffer index holding the current block input
+    const void* block_in = nullptr;
+    int block_len = 0;
+    for (int li = 0; li < nl; ++li) {
+        const Layer& L = h->layers[li];
+        const bool first = li == 0, last = li == nl - 1;
+        ConvGemmParams p{};
+        p.A = cur_in;
+        p.scale = L.scale;
+        p.shift = L.shift;
+        p.M = B * len[li];
+        p.N = L.cout;
+        p.K = L.K;
+        p.Kp = L.Kp;
+        p.T_out = len[li];
+        p.T_in = cur_len;
+        p.stride = L.stride;
+        p.dil = L.dil;
+        p.Ktap = L.Ktap;
+        p.lda = L.cin;
+        p.relu = L.relu ? 1 : 0;
+        p.ldy = L.cout;
+        p.W = dtype == VP3D_DTYPE_F32 ? (const void*)L.w32
+                                      : (dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh);
+        int out_buf = -1;
+        if (last) {
+            p.Y = y;
+        } else {
+            // pick a buffer that is neither the current input nor the block input
+            for (int bi = 0; bi < 3; ++bi) {
+                if (buf[bi] == cur_in || buf[bi] == block_in) continue;
+                out_buf = bi;
+                break;
+            }
+            p.Y = buf[out_buf];
+        }
+        if (L.residual) {
+            p.R = block_in;
+            p.R_T = block_len;
+            p.R_stride = L.res_stride;
+            p.R_off = L.res_off;
+            p.ldr = L.cout;
+        }
+        const Act a_type = first ? Act::F32 : act;
+        const Act o_type = last ? Act::F32 : act;
+
+        ProfEvent pe{};
+        if (h->profiling) {
+            pe.layer = li;
+            pe.a = get_event(h);
+            pe.b = get_event(h);
+            pe.flop = 2.0 * (double)p.M * (double)p.N * (double)p.K;
+            hipEventRecord(pe.a, s);
+        }
+        hipError_t e = launch_conv_gemm(p, a_type, o_type, act, s);
+        if (e != hipSuccess)
+            return fail(VP3D_ERR_HIP, std::string("conv layer ") + std::to_string(li) + ": " +
+                                          hipGetErrorString(e));
+        if (h->profiling) {
+            hipEventRecord(pe.b, s);
+            h->pending.push_back(pe);
+        }
+        // the k-conv of a block reads the block input; remember it for the 1x1's residual
+        if (!last && !L.residual && !first) {
+            block_in = cur_in;
+            block_len = cur_len;
+        }
+        if (first) {
+            // expand output is the first block's input
+        }
+        cur_in = p.Y;
+        cur_len = len[li];
+        (void)xin_buf;
+    }
+    return VP3D_OK;
+}
+
+int vp3d_profile_enable(vp3d_handle* h, int enable) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    h->profiling = enable != 0;
+    return VP3D_OK;
+}
+
+int vp3d_profile_reset(vp3d_handle* h) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    for (auto& e : h->pending) {
+        hipEventSynchronize(e.b);
+        h->free_events.push_back(e.a);
+        h->free_events.push_back(e.b);
+    }
+    h->pending.clear();
+    std::fill(h->prof_ms.begin(), h->prof_ms.end(), 0.0);
+    std::fill(h->prof_n.begin(), h->prof_n.end(), 0);
+    return VP3D_OK;
+}
+
+int vp3d_profile_read(vp3d_handle* h, double* ms_total, int64_t* launches, double* flop_last) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    for (auto& e : h->pending) {
+        HIP_TRY(hipEventSynchronize(e.b));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, e.a, e.b));
+        h->prof_ms[e.layer] += ms;
+        h->prof_n[e.layer] += 1;
+        h->prof_flop[e.layer] = e.flop;
+        h->free_events.push_back(e.a);
+        h->free_events.push_back(e.b);
+    }
+    h->pending.clear();
+    for (size_t i = 0; i < h->layers.size(); ++i) {
+        if (ms_total) ms_total[i] = h->prof_ms[i];
+        if (launches) launches[i] = h->prof_n[i];
+        if (flop_last) flop_last[i] = h->prof_flop[i];
+    }
+    return VP3D_OK;
+}
+
+// ---- on-device input path ----
+
+int vp3d_normalize_screen(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,
+                          void* stream) {
+    if (n_points < 0 || (n_points > 0 && (!x || !out))) return fail(VP3D_ERR_ARG, "bad pointer");
+    if (w <= 0) return fail(VP3D_ERR_ARG, "w must be positive");
+    HIP_TRY(launch_normalize_screen(x, n_points, w, h, out, false, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+int vp3d_image_coordinates(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,
+                           void* stream) {
+    if (n_points < 0 || (n_points > 0 && (!x || !out))) return fail(VP3D_ERR_ARG, "bad pointer");
+    if (w <= 0) return fail(VP3D_ERR_ARG, "w must be positive");
+    HIP_TRY(launch_normalize_screen(x, n_points, w, h, out, true, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+int vp3d_camera_matrices(const float* intr, const int32_t* frame_seq, const double* extr,
+                         int64_t n_frames, float* out, void* stream) {
+    if (n_frames < 0 || (n_frames > 0 && (!intr || !frame_seq || !extr || !out)))
+        return fail(VP3D_ERR_ARG, "bad pointer");
+    HIP_TRY(launch_camera_matrices(intr, frame_seq, extr, n_frames, out, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+int vp3d_world_to_camera(const float* X, int64_t n_points, const float* R_host, const float* t_host,
+                         float* out, void* stream) {
+    if (!R_host || !t_host) return fail(VP3D_ERR_ARG, "R / t is NULL");
+    if (n_points < 0 || (n_points > 0 && (!X || !out))) return fail(VP3D_ERR_ARG, "bad pointer");
+    HIP_TRY(launch_world_to_camera(X, n_points, R_host, t_host, out, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+int vp3d_gather_windows(const float* kps, int32_t f2, const float* cams, const int64_t* seq_off,
+                        const int32_t* seq_len, const int32_t* pairs, int32_t B, int32_t window,
+                        int32_t pad, int32_t causal_shift, float* out, void* stream) {
+    if (B < 0 || window <= 0 || f2 <= 0) return fail(VP3D_ERR_ARG, "bad sizes");
+    if (B > 0 && (!kps || !seq_off || !seq_len || !pairs || !out)) return fail(VP3D_ERR_ARG, "bad pointer");
+    HIP_TRY(launch_gather_windows(kps, f2, cams, seq_off, seq_len, pairs, B, window, pad,
+                                  causal_shift, out, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_points, double* acc,
+                          void* stream) {
+    if (n_points < 0 || (n_points > 0 && (!pred || !target || !acc)))
+        return fail(VP3D_ERR_ARG, "bad pointer");
+    HIP_TRY(launch_mpjpe_accumulate(pred, target, n_points, acc, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+}  // extern "C"

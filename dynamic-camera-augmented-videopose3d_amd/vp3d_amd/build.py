@@ -1,0 +1,74 @@
+"""In-tree build of libvp3d.so (the C-ABI of include/vp3d.h) for gfx950.
+
+Plain `hipcc` per translation unit, then one shared-library link.  Objects are
+rebuilt only when a source or header is newer than the object, so repeated
+builds are cheap.  The library lands next to this file so that it travels to
+the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT_PKG = os.path.dirname(PKG_DIR)                       # dynamic-camera-augmented-videopose3d_amd/
+REPO = os.path.dirname(ROOT_PKG)
+CSRC = os.path.join(ROOT_PKG, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+BUILD_DIR = os.path.join(ROOT_PKG, "build")
+LIB_PATH = os.path.join(PKG_DIR, "libvp3d.so")
+
+SOURCES = ["conv_gemm.hip", "preprocess.hip", "stream_step.hip", "vp3d_capi.cpp"]
+HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(INCLUDE, "vp3d.h")]
+ARCH = os.environ.get("VP3D_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-I", INCLUDE, "-I", CSRC,
+                "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-value",
+                "-Wno-unused-result"]
+
+
+def _newer(src_paths, dst):
+    if not os.path.exists(dst):
+        return True
+    t = os.path.getmtime(dst)
+    return any(os.path.getmtime(p) > t for p in src_paths)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n$ " + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    objs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        if not os.path.exists(src):
+            continue
+        obj = os.path.join(BUILD_DIR, s + ".o")
+        objs.append(obj)
+        if force or _newer([src] + HEADERS, obj):
+            if s.endswith(".hip"):
+                cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON_FLAGS + ["-c", src, "-o", obj]
+            else:
+                cmd = [HIPCC] + COMMON_FLAGS + ["-c", src, "-o", obj]
+            if verbose:
+                print("$", " ".join(cmd), flush=True)
+            out = _run(cmd)
+            if verbose and out.strip():
+                print(out)
+    if force or _newer(objs, LIB_PATH):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB_PATH] + objs
+        if verbose:
+            print("$", " ".join(cmd), flush=True)
+        _run(cmd)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

@@ -1,0 +1,176 @@
+/*
+ * vp3d.h — C-ABI of the MI355X-native VideoPose3D temporal lifter.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (Bart-Weil/Dynamic-Camera-Augmented-VideoPose3D, common/models/TemporalModel.py).
+ * The reference is pure Python, so it has no FFI of its own; every entry point
+ * below names the Python interface it replaces (file:line in the reference) and
+ * is bound from Python with ctypes.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  No torch types cross this boundary.
+ *   - "device" pointers are HIP device allocations on the handle's device;
+ *     "host" pointers are ordinary process memory.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream).
+ *   - Every function returns VP3D_OK (0) or a VP3D_ERR_* code; the message of the
+ *     last failure on the calling thread is available from vp3d_last_error().
+ *     The Python shim maps VP3D_ERR_ASSERT to AssertionError (the reference's
+ *     `assert` convention, TemporalModel.py:21,63-65) and everything else to
+ *     RuntimeError.
+ *   - Layouts are channel-last: a (B, T, J, F) pose tensor is already the
+ *     (B, T, J*F) activation matrix the first convolution consumes, and the
+ *     (B, T', J_out*3) output matrix is already the (B, T', J_out, 3) result.
+ */
+#ifndef VP3D_H
+#define VP3D_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VP3D_ABI_VERSION 1
+#define VP3D_MAX_BLOCKS 8
+
+/* status codes */
+#define VP3D_OK 0
+#define VP3D_ERR_ASSERT 1 /* shape / rank / config violation (reference: assert) */
+#define VP3D_ERR_ARG 2    /* bad pointer or argument                          */
+#define VP3D_ERR_HIP 3    /* HIP runtime failure                              */
+#define VP3D_ERR_OOM 4    /* device allocation failed                         */
+#define VP3D_ERR_STATE 5  /* handle misuse (wrong device, not reserved, ...)  */
+
+/* model variants (TemporalModel.py:79 and :141) */
+#define VP3D_VARIANT_DILATED 0    /* TemporalModel             */
+#define VP3D_VARIANT_STRIDED_1F 1 /* TemporalModelOptimized1f  */
+
+/* arithmetic type of the convolution stack */
+#define VP3D_DTYPE_F32 0  /* exact f32 MFMA (v_mfma_f32_16x16x4_f32), the parity path */
+#define VP3D_DTYPE_BF16 1 /* bf16 operands, f32 accumulate (v_mfma_f32_16x16x32_bf16) */
+#define VP3D_DTYPE_F16 2  /* f16 operands, f32 accumulate (v_mfma_f32_16x16x32_f16)   */
+
+/* Model configuration: the constructor arguments of TemporalModel /
+ * TemporalModelOptimized1f (TemporalModel.py:85-86, :152-153). */
+typedef struct vp3d_cfg {
+    int32_t num_joints_in;
+    int32_t in_features;
+    int32_t num_joints_out;
+    int32_t n_widths;                        /* len(filter_widths)                  */
+    int32_t filter_widths[VP3D_MAX_BLOCKS];  /* odd widths, e.g. 3,3,3,3,3          */
+    int32_t causal;                          /* 0/1                                 */
+    int32_t channels;                        /* e.g. 1024                           */
+    int32_t dense;                           /* 0/1 (dilated variant only)          */
+    int32_t variant;                         /* VP3D_VARIANT_*                      */
+    float bn_eps;                            /* BatchNorm1d eps (1e-5 in reference) */
+} vp3d_cfg;
+
+typedef struct vp3d_handle vp3d_handle;
+
+/* ---- lifecycle (replaces TemporalModel.__init__ + load_state_dict + .cuda()) ---- */
+
+/* Number of host weight arrays vp3d_create / vp3d_load_weights expect, in
+ * state_dict order (TemporalModel.py:32-33,102,113-119):
+ *   expand_conv.weight (C, J_in*F, w0)
+ *   expand_bn.{weight, bias, running_mean, running_var} (C each)
+ *   for i in 0..2*(n_widths-1)-1:
+ *       layers_conv.i.weight (C, C, k_i)
+ *       layers_bn.i.{weight, bias, running_mean, running_var}
+ *   shrink.weight (J_out*3, C, 1), shrink.bias (J_out*3)
+ * i.e. 5 + 10*(n_widths-1) + 2 arrays of float32, contiguous, PyTorch layout.
+ * Returns the count, or -1 on an invalid configuration. */
+int vp3d_weight_count(const vp3d_cfg* cfg);
+
+/* Validate cfg (odd widths: TemporalModel.py:20-21), fold every eval-mode
+ * BatchNorm into a per-channel (scale, shift) pair, pack the convolution
+ * weights tap-major for the MFMA kernels (f32 and bf16 copies) and upload them
+ * to the current HIP device.  `weights` are HOST pointers. */
+int vp3d_create(const vp3d_cfg* cfg, const float* const* weights, int n_weights, vp3d_handle** out);
+
+/* Re-pack and re-upload weights into an existing handle (load_state_dict,
+ * TemporalModel.py via nn.Module; called by run.py:416-417). Synchronous. */
+int vp3d_load_weights(vp3d_handle* h, const float* const* weights, int n_weights);
+
+int vp3d_destroy(vp3d_handle* h);
+
+/* ---- shape helpers (TemporalModel.py:40-60) ---- */
+int vp3d_receptive_field(const vp3d_handle* h);     /* 1 + 2*sum(pad)               */
+int vp3d_total_causal_shift(const vp3d_handle* h);  /* bit-compatible, quirk Q5     */
+/* Output frames for an input of T frames, or -1 if T is invalid for the variant. */
+int vp3d_out_frames(const vp3d_handle* h, int T);
+
+/* ---- forward (replaces TemporalModelBase.forward, TemporalModel.py:62-76) ---- */
+
+/* Allocate the activation workspace for (B, T, dtype) up front so that a later
+ * vp3d_forward with B' <= B, T' <= T allocates nothing (and can be captured into
+ * a hipGraph). */
+int vp3d_reserve(vp3d_handle* h, int B, int T, int dtype);
+
+/* Eval-mode forward.  x: device f32 (B, T, J_in, F) contiguous.
+ * y: device f32 (B, vp3d_out_frames(T), J_out, 3) contiguous, written here.
+ * Launches on `stream`; returns without synchronising. */
+int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream);
+
+/* ---- per-layer timing (HIP events recorded on the launch stream) ---- */
+int vp3d_profile_enable(vp3d_handle* h, int enable);
+/* Number of kernel launches one forward makes (conv layers incl. shrink). */
+int vp3d_layer_count(const vp3d_handle* h);
+/* Accumulated time (ms) and launch count per layer since the last reset, and
+ * the algorithmic FLOP of each layer's most recent launch.  Synchronises on
+ * the recorded events.  Arrays have vp3d_layer_count() entries. */
+int vp3d_profile_read(vp3d_handle* h, double* ms_total, int64_t* launches, double* flop_last);
+int vp3d_profile_reset(vp3d_handle* h);
+
+/* ---- on-device input path (common/camera.py, common/generators.py) ---- */
+
+/* normalize_screen_coordinates (camera.py:14-18): out = X/w*2 - [1, h/w] for
+ * n_points (x, y) pairs, with the reference's float64 promotion of the offset
+ * reproduced exactly (quirk Q6).  Device pointers, in-place allowed. */
+int vp3d_normalize_screen(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,
+                          void* stream);
+
+/* image_coordinates (camera.py:21-25): out = (X + [1, h/w]) * w / 2. */
+int vp3d_image_coordinates(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,
+                           void* stream);
+
+/* Per-frame camera matrices K @ E_t (generators.py:115-125, :180-190).
+ * intr: device f32 [fx, fy, cx, cy] per sequence (n_seq x 4); frame_seq: device
+ * int32 sequence id of each frame; extr: device f64 (n_frames, 3, 4) extrinsics;
+ * out: device f32 (n_frames, 12).  Evaluated in float64 like the reference's
+ * float32 @ float64 numpy matmul, then rounded once to f32. */
+int vp3d_camera_matrices(const float* intr, const int32_t* frame_seq, const double* extr,
+                         int64_t n_frames, float* out, void* stream);
+
+/* world_to_camera (camera.py:28-30 -> quaternion.py:10-35):
+ * out = qrot(qinverse(R), X - t) for n_points 3-vectors; R (4,) and t (3,) host
+ * values (one camera per call, like the reference). */
+int vp3d_world_to_camera(const float* X, int64_t n_points, const float* R_host,
+                         const float* t_host, float* out, void* stream);
+
+/* Window gather with edge padding (ChunkedGenerator.pad_chunk/next_epoch,
+ * generators.py:92-137; UnchunkedGenerator edge pad :193-198), fused with the
+ * trajectory concat (CamTransformer.py:187-190).
+ *   kps:      device f32 (n_frames, F2) normalised 2D keypoints (F2 = J*2)
+ *   cams:     device f32 (n_frames, 12) camera matrices or NULL (no concat)
+ *   seq_off:  device int64 first frame of each sequence; seq_len: device int32
+ *   pairs:    device int32 (B, 2) = (sequence id, first output frame start_3d)
+ *   out:      device f32 (B, window, F2 [+12])
+ * Window b covers frames [start_3d - pad - shift, start_3d - pad - shift + window)
+ * of its sequence, indices clamped to [0, len-1] ('edge' padding). */
+int vp3d_gather_windows(const float* kps, int32_t f2, const float* cams, const int64_t* seq_off,
+                        const int32_t* seq_len, const int32_t* pairs, int32_t B, int32_t window,
+                        int32_t pad, int32_t causal_shift, float* out, void* stream);
+
+/* mpjpe partial sums (loss.py:11-17): acc[0] += sum ||pred - target||_2 over
+ * n_points xyz triples, acc[1] += n_points.  acc: device f64[2] (caller zeroes). */
+int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_points, double* acc,
+                          void* stream);
+
+const char* vp3d_last_error(void);
+int vp3d_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VP3D_H */
