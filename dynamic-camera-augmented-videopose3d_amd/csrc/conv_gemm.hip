@@ -86,7 +86,14 @@ __device__ __forceinline__ int res_row(const ConvGemmParams& p, int m) {
     return b * p.R_T + t * p.R_stride + p.R_off;
 }
 
-// Scalar A element loader (general tap mapping, bounds-checked, zero fill).
+// A-operand addressing modes
+//   A_SCALAR  general tap mapping, one element at a time (bounds-checked, zero fill)
+//   A_PAIRS   one contiguous K segment per row (taps collapsed, dil == 1) of f32
+//             activations with an even row pitch: 8-byte loads, no division
+//             (the expand conv: K = w0 * J * F = 102 or 138)
+//   A_VEC     tap-aligned K tiles (Ktap % BK == 0): 16-byte loads
+enum : int { A_SCALAR = 0, A_PAIRS = 1, A_VEC = 2 };
+
 template <typename AT>
 __device__ __forceinline__ float load_a_scalar(const ConvGemmParams& p, int srow, int kk) {
     if (kk >= p.K) return 0.f;
@@ -96,7 +103,38 @@ __device__ __forceinline__ float load_a_scalar(const ConvGemmParams& p, int srow
     return to_f32(A[(int64_t)(srow + tap * p.dil) * p.lda + c]);
 }
 
-// Epilogue for one accumulator register: BN scale/shift, ReLU, residual add, store.
+// NE consecutive A elements of row `srow` starting at k index kk0 (NE % 2 == 0), as f32.
+template <typename AT, int AMODE, int NE>
+__device__ __forceinline__ void load_a_run(const ConvGemmParams& p, int srow, int kk0, bool valid,
+                                           float (&v)[NE]) {
+    if (!valid) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[e] = 0.f;
+        return;
+    }
+    if constexpr (AMODE == A_PAIRS) {
+        const float* row = (const float*)p.A + (int64_t)srow * p.lda;
+#pragma unroll
+        for (int e = 0; e < NE; e += 2) {
+            const int kk = kk0 + e;
+            if (kk < p.K) {
+                const float2 t = *(const float2*)(row + kk);
+                v[e] = t.x;
+                v[e + 1] = t.y;
+            } else {
+                v[e] = v[e + 1] = 0.f;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[e] = load_a_scalar<AT>(p, srow, kk0 + e);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Epilogues
+// ---------------------------------------------------------------------------
+// Scalar epilogue (any N): straight from the MFMA accumulator layout.
 template <typename OT>
 __device__ __forceinline__ void epi_store(const ConvGemmParams& p, int m, int n, float v,
                                           float sc, float sh) {
@@ -107,13 +145,116 @@ __device__ __forceinline__ void epi_store(const ConvGemmParams& p, int m, int n,
     ((OT*)p.Y)[(int64_t)m * p.ldy + n] = from_f32<OT>(v);
 }
 
+template <typename OT>
+__device__ __forceinline__ void epilogue_scalar(const ConvGemmParams& p, const f32x4 (&acc)[4][4],
+                                                int mw, int nw, int lane) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = nw + j * 16 + (lane & 15);
+        if (n >= p.N) continue;
+        const float sc = p.scale[n], sh = p.shift[n];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mw + i * 16 + (lane >> 4) * 4 + r;
+                if (m < p.M) epi_store<OT>(p, m, n, acc[i][j][r], sc, sh);
+            }
+    }
+}
+
+// Vector epilogue (N % 8 == 0): each wave transposes its 64x64 f32 accumulator
+// tile through its own LDS region (row pitch 68 floats: conflict-free writes),
+// then every lane owns 8 consecutive columns of a row: 16/32-byte residual loads
+// and output stores, whole 128-byte lines per 8 lanes.
+constexpr int kEpiLd = 68;
+
+template <typename OT, int PASS_ROWS>
+__device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x4 (&acc)[4][4],
+                                             float* stage, int mw, int nw, int lane) {
+    const int c8 = lane & 7;
+    const int n = nw + c8 * 8;
+    const bool nval = n < p.N;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sc[e] = nval ? p.scale[n + e] : 0.f;
+        sh[e] = nval ? p.shift[n + e] : 0.f;
+    }
+#pragma unroll
+    for (int pass = 0; pass < 64 / PASS_ROWS; ++pass) {
+#pragma unroll
+        for (int ii = 0; ii < PASS_ROWS / 16; ++ii) {
+            const int i = pass * (PASS_ROWS / 16) + ii;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    stage[(ii * 16 + (lane >> 4) * 4 + r) * kEpiLd + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PASS_ROWS / 8; ++q) {
+            const int row = q * 8 + (lane >> 3);
+            const int m = mw + pass * PASS_ROWS + row;
+            const f32x4 lo = *(const f32x4*)&stage[row * kEpiLd + c8 * 8];
+            const f32x4 hi = *(const f32x4*)&stage[row * kEpiLd + c8 * 8 + 4];
+            if (m < p.M && nval) {
+                float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    v[e] = __fadd_rn(__fmul_rn(v[e], sc[e]), sh[e]);
+                    if (p.relu) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                }
+                if (p.R) {
+                    const int64_t ro = (int64_t)res_row(p, m) * p.ldr + n;
+                    if constexpr (sizeof(OT) == 2) {
+                        const u32x4 rv = *(const u32x4*)((const OT*)p.R + ro);
+                        typedef OT ot8 __attribute__((ext_vector_type(8)));
+                        const ot8 r8 = __builtin_bit_cast(ot8, rv);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
+                    } else {
+                        const f32x4 r0 = *(const f32x4*)((const float*)p.R + ro);
+                        const f32x4 r1 = *(const f32x4*)((const float*)p.R + ro + 4);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            v[e] += r0[e];
+                            v[e + 4] += r1[e];
+                        }
+                    }
+                }
+                const int64_t yo = (int64_t)m * p.ldy + n;
+                if constexpr (sizeof(OT) == 2) {
+                    typedef OT ot8 __attribute__((ext_vector_type(8)));
+                    ot8 o;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] = (OT)v[e];
+                    *(u32x4*)((OT*)p.Y + yo) = __builtin_bit_cast(u32x4, o);
+                } else {
+                    *(f32x4*)((float*)p.Y + yo) = f32x4{v[0], v[1], v[2], v[3]};
+                    *(f32x4*)((float*)p.Y + yo + 4) = f32x4{v[4], v[5], v[6], v[7]};
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 16-bit operand family
 // ---------------------------------------------------------------------------
-template <typename AT, typename OT, typename CT, bool AVEC>
+constexpr int kH16Bk = 64;
+constexpr int kH16MainBytes = 2 * 2 * BM * kH16Bk * 2;        // [buf][A,B] bf16 tiles
+constexpr int kEpiBytes = 4 * 64 * kEpiLd * 4;                // 4 waves x 64 rows
+constexpr int kH16Smem = kH16MainBytes > kEpiBytes ? kH16MainBytes : kEpiBytes;
+
+template <typename AT, typename OT, typename CT, int AMODE, bool VEPI>
 __global__ __launch_bounds__(256) void conv_gemm_h16(ConvGemmParams p) {
-    constexpr int BK = 64;                    // 8 chunks of 8 elements per row
-    __shared__ __attribute__((aligned(16))) u32x4 smem[2][2][BM * BK / 8];  // [buf][A,B]
+    constexpr int BK = kH16Bk;  // 8 chunks of 8 elements per row
+    __shared__ __attribute__((aligned(16))) char smem_raw[kH16Smem];
+    u32x4* const s4 = (u32x4*)smem_raw;  // [buf][A,B][BM*BK/8]
+    constexpr int TILE = BM * BK / 8;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -142,8 +283,7 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(ConvGemmParams p) {
 
     u32x4 ra[4], rb[4];
     auto gload = [&](int k0) {
-        // A
-        if constexpr (AVEC) {
+        if constexpr (AMODE == A_VEC) {
             const int tap = k0 / p.Ktap;
             const int cin = k0 - tap * p.Ktap + ld_c * 8;
 #pragma unroll
@@ -166,9 +306,7 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(ConvGemmParams p) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 float v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    v[e] = mval[i] ? load_a_scalar<AT>(p, srow[i], k0 + ld_c * 8 + e) : 0.f;
+                load_a_run<AT, AMODE, 8>(p, srow[i], k0 + ld_c * 8, mval[i], v);
                 ra[i] = pack8<CT>(v);
             }
         }
@@ -184,8 +322,8 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(ConvGemmParams p) {
         for (int i = 0; i < 4; ++i) {
             const int r = ld_row + 32 * i;
             const int slot = r * 8 + (ld_c ^ (r & 7));
-            smem[buf][0][slot] = ra[i];
-            smem[buf][1][slot] = rb[i];
+            s4[(2 * buf) * TILE + slot] = ra[i];
+            s4[(2 * buf + 1) * TILE + slot] = rb[i];
         }
     };
 
@@ -211,12 +349,12 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(ConvGemmParams p) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = wr * 64 + i * 16 + (lane & 15);
-                af[i] = smem[cur][0][r * 8 + (c ^ (r & 7))];
+                af[i] = s4[(2 * cur) * TILE + r * 8 + (c ^ (r & 7))];
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int r = wc * 64 + j * 16 + (lane & 15);
-                bfm[j] = smem[cur][1][r * 8 + (c ^ (r & 7))];
+                bfm[j] = s4[(2 * cur + 1) * TILE + r * 8 + (c ^ (r & 7))];
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -228,30 +366,27 @@ __global__ __launch_bounds__(256) void conv_gemm_h16(ConvGemmParams p) {
         cur ^= 1;
     }
 
-    // epilogue: D(row = (lane>>4)*4 + r, col = lane & 15) of each 16x16 block
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wc * 64 + j * 16 + (lane & 15);
-        if (n >= p.N) continue;
-        const float sc = p.scale[n], sh = p.shift[n];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wr * 64 + i * 16 + (lane >> 4) * 4 + r;
-                if (m < p.M) epi_store<OT>(p, m, n, acc[i][j][r], sc, sh);
-            }
-        }
-    }
+    const int mw = m0 + wr * 64, nw = n0 + wc * 64;
+    if constexpr (VEPI)
+        epilogue_vec<OT, 64>(p, acc, (float*)smem_raw + wid * 64 * kEpiLd, mw, nw, lane);
+    else
+        epilogue_scalar<OT>(p, acc, mw, nw, lane);
 }
 
 // ---------------------------------------------------------------------------
 // exact f32 family
 // ---------------------------------------------------------------------------
-template <bool AVEC>
+constexpr int kF32Bk = 16;
+constexpr int kF32MainBytes = 2 * 2 * BM * kF32Bk * 4;
+constexpr int kF32EpiBytes = 4 * 32 * kEpiLd * 4;  // two passes of 32 rows per wave
+constexpr int kF32Smem = kF32MainBytes > kF32EpiBytes ? kF32MainBytes : kF32EpiBytes;
+
+template <int AMODE, bool VEPI>
 __global__ __launch_bounds__(256) void conv_gemm_f32(ConvGemmParams p) {
-    constexpr int BK = 16;  // 4 chunks of 4 floats per row
-    __shared__ __attribute__((aligned(16))) f32x4 smem[2][2][BM * BK / 4];
+    constexpr int BK = kF32Bk;  // 4 chunks of 4 floats per row
+    __shared__ __attribute__((aligned(16))) char smem_raw[kF32Smem];
+    f32x4* const s4 = (f32x4*)smem_raw;  // [buf][A,B][BM*BK/4]
+    constexpr int TILE = BM * BK / 4;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -281,7 +416,7 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(ConvGemmParams p) {
 
     f32x4 ra[2], rb[2];
     auto gload = [&](int k0) {
-        if constexpr (AVEC) {
+        if constexpr (AMODE == A_VEC) {
             const int tap = k0 / p.Ktap;
             const int cin = k0 - tap * p.Ktap + ld_c * 4;
 #pragma unroll
@@ -290,10 +425,11 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(ConvGemmParams p) {
                                 : f32x4{0.f, 0.f, 0.f, 0.f};
         } else {
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    ra[i][e] = mval[i] ? load_a_scalar<float>(p, srow[i], k0 + ld_c * 4 + e) : 0.f;
+            for (int i = 0; i < 2; ++i) {
+                float v[4];
+                load_a_run<float, AMODE, 4>(p, srow[i], k0 + ld_c * 4, mval[i], v);
+                ra[i] = f32x4{v[0], v[1], v[2], v[3]};
+            }
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -306,8 +442,8 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(ConvGemmParams p) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int r = ld_row + 64 * i;
-            smem[buf][0][swz(r, ld_c)] = ra[i];
-            smem[buf][1][swz(r, ld_c)] = rb[i];
+            s4[(2 * buf) * TILE + swz(r, ld_c)] = ra[i];
+            s4[(2 * buf + 1) * TILE + swz(r, ld_c)] = rb[i];
         }
     };
 
@@ -328,9 +464,9 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(ConvGemmParams p) {
         f32x4 af[4], bfm[4];
         const int c = lane >> 4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = smem[cur][0][swz(wr * 64 + i * 16 + (lane & 15), c)];
+        for (int i = 0; i < 4; ++i) af[i] = s4[(2 * cur) * TILE + swz(wr * 64 + i * 16 + (lane & 15), c)];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bfm[j] = smem[cur][1][swz(wc * 64 + j * 16 + (lane & 15), c)];
+        for (int j = 0; j < 4; ++j) bfm[j] = s4[(2 * cur + 1) * TILE + swz(wc * 64 + j * 16 + (lane & 15), c)];
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -343,38 +479,49 @@ __global__ __launch_bounds__(256) void conv_gemm_f32(ConvGemmParams p) {
         cur ^= 1;
     }
 
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wc * 64 + j * 16 + (lane & 15);
-        if (n >= p.N) continue;
-        const float sc = p.scale[n], sh = p.shift[n];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wr * 64 + i * 16 + (lane >> 4) * 4 + r;
-                if (m < p.M) epi_store<float>(p, m, n, acc[i][j][r], sc, sh);
-            }
-    }
+    const int mw = m0 + wr * 64, nw = n0 + wc * 64;
+    if constexpr (VEPI)
+        epilogue_vec<float, 32>(p, acc, (float*)smem_raw + wid * 32 * kEpiLd, mw, nw, lane);
+    else
+        epilogue_scalar<float>(p, acc, mw, nw, lane);
 }
 
-template <typename AT, typename OT, typename CT>
-hipError_t launch_h16(const ConvGemmParams& p, bool avec, dim3 grid, hipStream_t s) {
-    if (avec)
-        hipLaunchKernelGGL((conv_gemm_h16<AT, OT, CT, true>), grid, dim3(256), 0, s, p);
+template <typename AT, typename OT, typename CT, int AMODE>
+hipError_t launch_h16_v(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t s) {
+    if (vepi)
+        hipLaunchKernelGGL((conv_gemm_h16<AT, OT, CT, AMODE, true>), grid, dim3(256), 0, s, p);
     else
-        hipLaunchKernelGGL((conv_gemm_h16<AT, OT, CT, false>), grid, dim3(256), 0, s, p);
+        hipLaunchKernelGGL((conv_gemm_h16<AT, OT, CT, AMODE, false>), grid, dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
-template <typename CT>
-hipError_t launch_h16_dispatch(const ConvGemmParams& p, Act a, Act o, bool avec, dim3 grid,
-                               hipStream_t s) {
-    if (a == Act::F32 && o == Act::F32) return launch_h16<float, float, CT>(p, avec, grid, s);
-    if (a == Act::F32) return launch_h16<float, CT, CT>(p, avec, grid, s);
-    if (o == Act::F32) return launch_h16<CT, float, CT>(p, avec, grid, s);
-    return launch_h16<CT, CT, CT>(p, avec, grid, s);
+template <typename AT, typename OT, typename CT>
+hipError_t launch_h16(const ConvGemmParams& p, int amode, bool vepi, dim3 grid, hipStream_t s) {
+    if (amode == A_VEC) return launch_h16_v<AT, OT, CT, A_VEC>(p, vepi, grid, s);
+    if constexpr (sizeof(AT) == 4)
+        if (amode == A_PAIRS) return launch_h16_v<AT, OT, CT, A_PAIRS>(p, vepi, grid, s);
+    return launch_h16_v<AT, OT, CT, A_SCALAR>(p, vepi, grid, s);
 }
+
+template <typename CT>
+hipError_t launch_h16_dispatch(const ConvGemmParams& p, Act a, Act o, int amode, bool vepi,
+                               dim3 grid, hipStream_t s) {
+    if (a == Act::F32 && o == Act::F32) return launch_h16<float, float, CT>(p, amode, vepi, grid, s);
+    if (a == Act::F32) return launch_h16<float, CT, CT>(p, amode, vepi, grid, s);
+    if (o == Act::F32) return launch_h16<CT, float, CT>(p, amode, vepi, grid, s);
+    return launch_h16<CT, CT, CT>(p, amode, vepi, grid, s);
+}
+
+template <int AMODE>
+hipError_t launch_f32(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t s) {
+    if (vepi)
+        hipLaunchKernelGGL((conv_gemm_f32<AMODE, true>), grid, dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((conv_gemm_f32<AMODE, false>), grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+bool aligned(const void* ptr, uintptr_t a) { return (reinterpret_cast<uintptr_t>(ptr) & (a - 1)) == 0; }
 
 }  // namespace
 
@@ -384,22 +531,28 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     const int ntm = (p.M + BM - 1) / BM;
     const int ntn = (p.N + BN - 1) / BN;
     const dim3 grid(ntm * ntn);
+    const bool contiguous = p.Ktap == p.K;  // taps collapsed into one K segment
+    const int oes = out_type == Act::F32 ? 4 : 2;
+    const bool vepi = (p.N % 8 == 0) && (p.ldy % 8 == 0) && aligned(p.Y, 16) &&
+                      (!p.R || ((p.ldr % 8 == 0) && aligned(p.R, 16))) && oes > 0;
     if (compute == Act::F32) {
         if (a_type != Act::F32 || out_type != Act::F32) return hipErrorInvalidValue;
-        const bool avec = (p.Ktap % 16 == 0) && (p.lda % 4 == 0) &&
-                          ((reinterpret_cast<uintptr_t>(p.A) & 15) == 0);
-        if (avec)
-            hipLaunchKernelGGL((conv_gemm_f32<true>), grid, dim3(256), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_f32<false>), grid, dim3(256), 0, stream, p);
-        return hipGetLastError();
+        if ((p.Ktap % kF32Bk == 0) && (p.lda % 4 == 0) && aligned(p.A, 16))
+            return launch_f32<A_VEC>(p, vepi, grid, stream);
+        if (contiguous && (p.lda % 2 == 0) && (p.K % 2 == 0) && aligned(p.A, 8))
+            return launch_f32<A_PAIRS>(p, vepi, grid, stream);
+        return launch_f32<A_SCALAR>(p, vepi, grid, stream);
     }
     if (a_type != Act::F32 && a_type != compute) return hipErrorInvalidValue;
     if (out_type != Act::F32 && out_type != compute) return hipErrorInvalidValue;
-    const bool avec = (p.Ktap % 64 == 0) && (p.lda % 8 == 0) &&
-                      ((reinterpret_cast<uintptr_t>(p.A) & 15) == 0);
-    if (compute == Act::BF16) return launch_h16_dispatch<bf16>(p, a_type, out_type, avec, grid, stream);
-    return launch_h16_dispatch<f16>(p, a_type, out_type, avec, grid, stream);
+    const int aes = a_type == Act::F32 ? 4 : 2;
+    int amode = A_SCALAR;
+    if ((p.Ktap % kH16Bk == 0) && (p.lda % 8 == 0) && aligned(p.A, 16))
+        amode = A_VEC;
+    else if (aes == 4 && contiguous && (p.lda % 2 == 0) && (p.K % 2 == 0) && aligned(p.A, 8))
+        amode = A_PAIRS;
+    if (compute == Act::BF16) return launch_h16_dispatch<bf16>(p, a_type, out_type, amode, vepi, grid, stream);
+    return launch_h16_dispatch<f16>(p, a_type, out_type, amode, vepi, grid, stream);
 }
 
 }  // namespace vp3d
