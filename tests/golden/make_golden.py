@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Generate the golden parity vectors by running the REFERENCE itself.
+
+Run in the build container only (the reference is not on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+It imports the reference's own modules read-only (common.models.TemporalModel,
+common.generators, common.camera, common.quaternion, common.loss), feeds them
+synthetic inputs and weights from vp3d_amd.synth (seeded counter hash, so the
+1024-channel weights are re-created by the tests instead of being stored), and
+writes small .npz fixtures next to this script.  Nothing of the reference's code
+is copied: the fixtures hold inputs and the reference's outputs only.
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+PKG = os.path.join(REPO, "dynamic-camera-augmented-videopose3d_amd")
+REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+
+# `common` must resolve to the reference (a namespace package there, so our
+# regular package must not be on sys.path); vp3d_amd.synth is loaded by file path.
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from common import camera as ref_camera  # noqa: E402
+from common import generators as ref_gen  # noqa: E402
+from common import loss as ref_loss  # noqa: E402
+from common.models import TemporalModel as ref_tm  # noqa: E402
+import importlib.util  # noqa: E402
+
+_spec = importlib.util.spec_from_file_location("vp3d_synth", os.path.join(PKG, "vp3d_amd", "synth.py"))
+synth = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(synth)
+
+assert os.path.realpath(ref_tm.__file__).startswith(os.path.realpath(REF)), ref_tm.__file__
+
+torch.set_num_threads(8)
+MANIFEST = {}
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    h = hashlib.sha256(open(path, "rb").read()).hexdigest()
+    MANIFEST[name] = {"bytes": os.path.getsize(path), "sha256": h,
+                      "arrays": {k: list(np.asarray(v).shape) for k, v in arrays.items()}}
+    print(f"{name}: {os.path.getsize(path) / 1024:.1f} KiB")
+
+
+def build_ref_model(strided, fw, causal=False, channels=1024, jin=17, jout=17, dense=False, seed=0):
+    if strided:
+        m = ref_tm.TemporalModelOptimized1f(jin, 2, jout, list(fw), causal=causal, channels=channels)
+    else:
+        m = ref_tm.TemporalModel(jin, 2, jout, list(fw), causal=causal, channels=channels, dense=dense)
+    keys = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    sd = synth.lifter_state_dict(keys, seed=seed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.eval()
+    return m, sd, keys
+
+
+def model_case(name, strided, fw, B, T, causal=False, channels=1024, jin=17, dense=False,
+               store_weights=False, seed=0):
+    m, sd, keys = build_ref_model(strided, fw, causal, channels, jin=jin, dense=dense, seed=seed)
+    x = synth.normalized_windows(seed + 1, name, B, T, n_joints=jin)
+    with torch.no_grad():
+        y = m(torch.from_numpy(x)).numpy()
+    meta = dict(strided=strided, fw=list(fw), causal=causal, channels=channels, jin=jin,
+                dense=dense, seed=seed, weights_sha256=synth.state_dict_sha256(sd),
+                receptive_field=m.receptive_field(), total_causal_shift=m.total_causal_shift(),
+                pad=list(m.pad), causal_shift=list(m.causal_shift),
+                n_params=int(sum(p.numel() for p in m.parameters())),
+                keys=[k for k, _ in keys], shapes=[list(s) for _, s in keys])
+    arrays = dict(x=x, y=y, meta=np.array(json.dumps(meta)))
+    if store_weights:
+        for k, v in sd.items():
+            arrays["w/" + k] = v
+    save(name, **arrays)
+
+
+def model_goldens():
+    F3, F5 = (3, 3, 3), (3, 3, 3, 3, 3)
+    model_case("opt1f_243_fp32", True, F5, 8, 243)
+    model_case("opt1f_243_causal_fp32", True, F5, 4, 243, causal=True)
+    model_case("seq_243_fp32", False, F5, 1, 400)
+    model_case("seq_243_causal_fp32", False, F5, 1, 300, causal=True)
+    model_case("seq_27_fp32", False, F3, 2, 300)
+    model_case("traj46_243_fp32", True, F5, 4, 243, jin=23)
+    model_case("small_dilated_c64", False, F3, 3, 60, channels=64, store_weights=True)
+    model_case("small_opt1f_c64", True, F3, 5, 27, channels=64, store_weights=True)
+    model_case("small_dense_c64", False, F3, 2, 50, channels=64, dense=True, store_weights=True)
+    model_case("small_causal_c64", False, (3, 5, 3), 2, 80, channels=64, causal=True,
+               store_weights=True)
+
+
+def cams_for(name, T):
+    E = synth.camera_extrinsics(2, name, T)
+    return {"intrinsics": dict(synth.CMU_INTRINSICS),
+            "extrinsics": E,
+            "cam_velocity": np.array([0.1, 0.0, 0.0]),
+            "cam_acceleration": np.array([0.0, 0.01, 0.0]),
+            "cam_angular_velocity": np.array([0.0, 0.0, 0.2]),
+            "cam_angular_acceleration": np.array([0.0, 0.0, 0.0])}
+
+
+def generator_goldens():
+    lens = [300, 90, 40]
+    pad, B = 121, 8
+    kps = [ref_camera.normalize_screen_coordinates(synth.keypoint_tracks(1, f"g{i}", n), 1280, 720)
+           .astype(np.float32) for i, n in enumerate(lens)]
+    p3d = [synth.gt_poses(3, f"g{i}", n) for i, n in enumerate(lens)]
+    cams = [cams_for(f"g{i}", n) for i, n in enumerate(lens)]
+    arrays = {}
+    for i in range(len(lens)):
+        arrays[f"kps{i}"] = kps[i]
+        arrays[f"p3d{i}"] = p3d[i]
+        arrays[f"extr{i}"] = cams[i]["extrinsics"]
+    for causal in (0, 1):
+        shift = pad if causal else 0
+        gen = ref_gen.UnchunkedGenerator(cams, p3d, kps, pad=pad, causal_shift=shift)
+        for j, (bc, b3, b2, info) in enumerate(gen.next_epoch()):
+            arrays[f"unchunked_c{causal}_cam{j}"] = bc.astype(np.float32)
+            arrays[f"unchunked_c{causal}_2d{j}"] = b2
+        cg = ref_gen.ChunkedGenerator(B, cams, p3d, kps, 1, pad=pad, causal_shift=shift,
+                                      shuffle=True, random_seed=1234)
+        arrays[f"chunked_c{causal}_pairs"] = np.array(cg.next_pairs()[1], dtype=np.int64)
+        # Q2: the generator yields its whole (reused) buffer; record the first two
+        # batches and the last (partial, with stale rows) one
+        cg2 = ref_gen.ChunkedGenerator(B, cams, p3d, kps, 1, pad=pad, causal_shift=shift,
+                                       shuffle=True, random_seed=1234)
+        for bi, (bc, b3, b2) in enumerate(cg2.next_epoch()):
+            if bi in (0, 1, cg2.num_batches - 1):
+                arrays[f"chunked_c{causal}_b{bi}_cam"] = bc.copy()
+                arrays[f"chunked_c{causal}_b{bi}_3d"] = b3.copy()
+                arrays[f"chunked_c{causal}_b{bi}_2d"] = b2.copy()
+        arrays[f"chunked_c{causal}_num_batches"] = np.array(cg2.num_batches)
+    arrays["meta"] = np.array(json.dumps(dict(lens=lens, pad=pad, batch_size=B, seed=1234)))
+    save("generators", **arrays)
+
+
+def camera_goldens():
+    a = {}
+    X = synth.keypoint_tracks(1, "cam", 64, 17)
+    for (w, h) in ((1280, 720), (1000, 1002), (1000, 1000)):
+        n = ref_camera.normalize_screen_coordinates(X, w, h)
+        a[f"norm_in_{w}x{h}"] = X
+        a[f"norm_out_{w}x{h}"] = n  # float64 (reference promotion, quirk Q6)
+        a[f"img_out_{w}x{h}"] = ref_camera.image_coordinates(n.astype(np.float32), w, h)
+    P = synth.normal(4, "w2c", (50, 17, 3), 1.0).astype(np.float32)
+    q = synth.normal(4, "w2c/q", (4,), 1.0)
+    q = (q / np.linalg.norm(q)).astype(np.float32)
+    t = synth.normal(4, "w2c/t", (3,), 1.0).astype(np.float32)
+    a["w2c_X"], a["w2c_R"], a["w2c_t"] = P, q, t
+    a["w2c_out"] = ref_camera.world_to_camera(P, R=q, t=t)
+    a["c2w_out"] = ref_camera.camera_to_world(a["w2c_out"].astype(np.float32), R=q, t=t)
+    save("camera", **a)
+
+
+def loss_goldens():
+    a = {}
+    pred = synth.normal(5, "pred", (2, 40, 17, 3), 0.2).astype(np.float32)
+    tgt = synth.normal(5, "tgt", (2, 40, 17, 3), 0.2).astype(np.float32)
+    a["pred"], a["tgt"] = pred, tgt
+    a["mpjpe"] = np.array(ref_loss.mpjpe(torch.from_numpy(pred), torch.from_numpy(tgt)).item())
+    a["n_mpjpe"] = np.array(ref_loss.n_mpjpe(torch.from_numpy(pred), torch.from_numpy(tgt)).item())
+    p2 = pred.reshape(-1, 17, 3)
+    t2 = tgt.reshape(-1, 17, 3)
+    a["p_mpjpe"] = np.array(ref_loss.p_mpjpe(p2.copy(), t2.copy()))
+    a["mpjve"] = np.array(ref_loss.mean_velocity_error(p2, t2))
+    save("loss", **a)
+
+
+if __name__ == "__main__":
+    model_goldens()
+    generator_goldens()
+    camera_goldens()
+    loss_goldens()
+    env = dict(torch=torch.__version__, numpy=np.__version__, python=sys.version.split()[0],
+               reference=REF)
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump({"environment": env, "fixtures": MANIFEST}, f, indent=1, sort_keys=True)
+    print("total KiB", sum(v["bytes"] for v in MANIFEST.values()) / 1024)
