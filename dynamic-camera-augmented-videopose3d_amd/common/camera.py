@@ -1,0 +1,51 @@
+"""Drop-in for the reference's ``common/camera.py`` hot-path helpers, on device.
+
+normalize_screen_coordinates (camera.py:14-18), image_coordinates (:21-25),
+world_to_camera (:28-30) and camera_to_world (:33-34) run as libvp3d kernels.
+HIP tensors stay on device; numpy arrays (the reference's calling convention at
+dataset-load time, run.py:78,117,123) are moved to the current device, computed
+there and returned as float32 numpy — exactly the values run.py stores (the
+reference computes the offset in float64 and writes the result back into its
+float32 arrays, quirk Q6).  The H36M distortion projections (:37-90) are
+offline-prep only and out of scope.
+"""
+import numpy as np
+import torch
+
+from vp3d_amd import pipeline as _P
+
+
+def _to_dev(X):
+    if isinstance(X, torch.Tensor):
+        return X, False
+    return torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).cuda(), True
+
+
+def normalize_screen_coordinates(X, w, h):
+    assert X.shape[-1] == 2
+    t, host = _to_dev(X)
+    out = _P.normalize_screen(t, w, h)
+    return out.cpu().numpy() if host else out
+
+
+def image_coordinates(X, w, h):
+    assert X.shape[-1] == 2
+    t, host = _to_dev(X)
+    out = _P.image_coordinates(t, w, h)
+    return out.cpu().numpy() if host else out
+
+
+def world_to_camera(X, R, t):
+    Xd, host = _to_dev(X)
+    out = _P.world_to_camera(Xd, R, t)
+    return out.cpu().numpy() if host else out
+
+
+def camera_to_world(X, R, t):
+    # qrot(R, X) + t == world_to_camera with the inverse rotation and no translation
+    R = np.asarray(R, dtype=np.float32)
+    Rinv = np.array([R[0], -R[1], -R[2], -R[3]], dtype=np.float32)
+    Xd, host = _to_dev(X)
+    out = _P.world_to_camera(Xd, Rinv, np.zeros(3, np.float32)) + torch.as_tensor(
+        np.asarray(t, dtype=np.float32), device=Xd.device)
+    return out.cpu().numpy() if host else out

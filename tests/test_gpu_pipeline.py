@@ -1,0 +1,130 @@
+"""GPU parity of the on-device input path against the reference goldens.
+
+Bar: bit-exact for the index/copy work (window gather, edge padding) and for
+the arithmetic the reference evaluates order-independently (normalisation with
+its float64 offset, K @ E with two non-zero products per entry); world_to_camera
+and mpjpe within 2 ulp-scale tolerances (torch-CPU's cross product / mean may use
+FMA and a different reduction order).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from vp3d_amd import synth
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+
+
+@pytest.mark.parametrize("wh", [(1280, 720), (1000, 1002), (1000, 1000)])
+def test_normalize_bit_exact(wh):
+    from common.camera import image_coordinates, normalize_screen_coordinates
+    g = load("camera")
+    w, h = wh
+    X = torch.from_numpy(g[f"norm_in_{w}x{h}"]).cuda()
+    out = normalize_screen_coordinates(X, w, h).cpu().numpy()
+    assert np.array_equal(out, g[f"norm_out_{w}x{h}"].astype(np.float32))
+    back = image_coordinates(torch.from_numpy(g[f"norm_out_{w}x{h}"].astype(np.float32)).cuda(), w, h)
+    assert np.array_equal(back.cpu().numpy(), g[f"img_out_{w}x{h}"].astype(np.float32))
+    # numpy calling convention (run.py:117)
+    assert np.array_equal(normalize_screen_coordinates(g[f"norm_in_{w}x{h}"], w, h),
+                          g[f"norm_out_{w}x{h}"].astype(np.float32))
+
+
+def test_world_to_camera():
+    from common.camera import camera_to_world, world_to_camera
+    g = load("camera")
+    out = world_to_camera(g["w2c_X"], R=g["w2c_R"], t=g["w2c_t"])
+    np.testing.assert_allclose(out, g["w2c_out"], rtol=0, atol=2e-6)
+    frac = np.mean(out == g["w2c_out"])
+    print(f"world_to_camera bit-exact fraction {frac:.4f}")
+    back = camera_to_world(g["w2c_out"].astype(np.float32), R=g["w2c_R"], t=g["w2c_t"])
+    np.testing.assert_allclose(back, g["c2w_out"], rtol=0, atol=2e-6)
+
+
+def _gen():
+    g = load("generators")
+    meta = json.loads(str(g["meta"]))
+    n = len(meta["lens"])
+    kps = [g[f"kps{i}"] for i in range(n)]
+    p3d = [g[f"p3d{i}"] for i in range(n)]
+    cams = [{"intrinsics": dict(synth.CMU_INTRINSICS), "extrinsics": g[f"extr{i}"],
+             "cam_velocity": np.zeros(3)} for i in range(n)]
+    return g, meta, kps, p3d, cams
+
+
+@pytest.mark.parametrize("causal", [0, 1])
+def test_unchunked_generator_bit_exact(causal):
+    from common.generators import UnchunkedGenerator
+    g, meta, kps, p3d, cams = _gen()
+    pad = meta["pad"]
+    gen = UnchunkedGenerator(cams, p3d, kps, pad=pad, causal_shift=pad if causal else 0)
+    for j, (bc, b3, b2, info) in enumerate(gen.next_epoch()):
+        assert np.array_equal(b2.cpu().numpy(), g[f"unchunked_c{causal}_2d{j}"])
+        assert np.array_equal(bc.cpu().numpy(), g[f"unchunked_c{causal}_cam{j}"])
+        assert np.array_equal(b3.cpu().numpy()[0], p3d[j])
+    assert j == len(kps) - 1
+
+
+@pytest.mark.parametrize("causal", [0, 1])
+def test_chunked_generator_bit_exact(causal):
+    from common.generators import ChunkedGenerator
+    g, meta, kps, p3d, cams = _gen()
+    pad, B = meta["pad"], meta["batch_size"]
+    gen = ChunkedGenerator(B, cams, p3d, kps, 1, pad=pad, causal_shift=pad if causal else 0,
+                           shuffle=True, random_seed=1234)
+    nb = 0
+    for bi, (bc, b3, b2) in enumerate(gen.next_epoch()):
+        nb += 1
+        key = f"chunked_c{causal}_b{bi}"
+        if key + "_2d" not in g.files:
+            continue
+        n = b2.shape[0]  # the last batch is trimmed (quirk Q2); compare the valid rows
+        assert np.array_equal(b2.cpu().numpy(), g[key + "_2d"][:n].astype(np.float32))
+        assert np.array_equal(bc.cpu().numpy(), g[key + "_cam"][:n].astype(np.float32))
+        assert np.array_equal(b3.cpu().numpy(), g[key + "_3d"][:n].astype(np.float32))
+    assert nb == int(g[f"chunked_c{causal}_num_batches"])
+
+
+def test_trajectory_concat_gather():
+    from common.generators import ChunkedGenerator
+    g, meta, kps, p3d, cams = _gen()
+    pad, B = meta["pad"], meta["batch_size"]
+    gen = ChunkedGenerator(B, cams, p3d, kps, 1, pad=pad, trajectory=True)
+    bc, b3, b2 = next(iter(gen.next_epoch()))
+    ref = g["chunked_c0_b0_2d"].astype(np.float32).reshape(B, 2 * pad + 1, -1)
+    cam = g["chunked_c0_b0_cam"].astype(np.float32).reshape(B, 2 * pad + 1, 12)
+    want = np.concatenate([ref, cam], axis=-1).reshape(B, 2 * pad + 1, 23, 2)
+    assert np.array_equal(b2.cpu().numpy(), want)
+
+
+def test_mpjpe_kernel():
+    from common.loss import mpjpe
+    g = load("loss")
+    v = mpjpe(torch.from_numpy(g["pred"]).cuda(), torch.from_numpy(g["tgt"]).cuda()).item()
+    assert abs(v - float(g["mpjpe"])) <= 1e-6 * abs(float(g["mpjpe"]))
+
+
+def test_gather_edge_cases():
+    """Windows entirely before / after a short sequence clamp to its first / last frame;
+    a 1-frame sequence replicates."""
+    from vp3d_amd.pipeline import DeviceSequences
+    seqs = [np.arange(5 * 4, dtype=np.float32).reshape(5, 2, 2),
+            np.full((1, 2, 2), 7.0, np.float32)]
+    ds = DeviceSequences(seqs)
+    pairs = torch.tensor([[0, -10], [0, 100], [1, 0], [0, 2]], dtype=torch.int32, device="cuda")
+    out = ds.gather(pairs, 7, 3, "2d").cpu().numpy()
+    s0 = seqs[0].reshape(5, 4)
+    assert np.array_equal(out[0], np.repeat(s0[:1], 7, 0))
+    assert np.array_equal(out[1], np.repeat(s0[-1:], 7, 0))
+    assert np.array_equal(out[2], np.full((7, 4), 7.0, np.float32))
+    assert np.array_equal(out[3], s0[np.clip(np.arange(-1, 6), 0, 4)])
+    empty = ds.gather(pairs[:0], 7, 3, "2d")
+    assert empty.shape == (0, 7, 4)
