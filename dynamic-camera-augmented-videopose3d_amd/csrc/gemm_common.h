@@ -1,0 +1,226 @@
+// Device-side building blocks shared by the conv-GEMM kernel families
+// (conv_gemm.hip: 128x128 tiles; conv_gemm_big.hip: 256x256 LDS-DMA tiles).
+#pragma once
+#include "kernels.h"
+
+// No silent FMA contraction in the epilogues: the BatchNorm affine is applied
+// as ATen's CPU kernel applies it (x * alpha, then + beta, two roundings).
+#pragma clang fp contract(off)
+
+namespace vp3d {
+namespace gemm {
+
+typedef __bf16 bf16;
+typedef _Float16 f16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    // bijective round-robin inverse (cdna_hip_programming.md §5 "XCD swizzle must be bijective")
+    const int xcd = bid & 7;
+    const int q = nwg >> 3, r = nwg & 7;
+    const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (bid >> 3);
+}
+
+template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
+
+template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
+
+template <typename CT> struct Pack8;
+template <> struct Pack8<bf16> { typedef bf16x8 type; };
+template <> struct Pack8<f16> { typedef f16x8 type; };
+
+template <typename CT>
+__device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
+    typename Pack8<CT>::type r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = (CT)v[e];
+    return __builtin_bit_cast(u32x4, r);
+}
+
+template <typename CT>
+__device__ __forceinline__ f32x4 mfma16(u32x4 a, u32x4 b, f32x4 c);
+template <>
+__device__ __forceinline__ f32x4 mfma16<bf16>(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma16<f16>(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int src_row(const ConvGemmParams& p, int m) {
+    const int b = m / p.T_out;
+    const int t = m - b * p.T_out;
+    return b * p.T_in + t * p.stride;
+}
+
+__device__ __forceinline__ int res_row(const ConvGemmParams& p, int m) {
+    const int b = m / p.T_out;
+    const int t = m - b * p.T_out;
+    return b * p.R_T + t * p.R_stride + p.R_off;
+}
+
+// A-operand addressing modes
+//   A_SCALAR  general tap mapping, one element at a time (bounds-checked, zero fill)
+//   A_PAIRS   one contiguous K segment per row (taps collapsed, dil == 1) of f32
+//             activations with an even row pitch: 8-byte loads, no division
+//             (the expand conv: K = w0 * J * F = 102 or 138)
+//   A_VEC     tap-aligned K tiles (Ktap % BK == 0): 16-byte loads
+enum : int { A_SCALAR = 0, A_PAIRS = 1, A_VEC = 2 };
+
+template <typename AT>
+__device__ __forceinline__ float load_a_scalar(const ConvGemmParams& p, int srow, int kk) {
+    if (kk >= p.K) return 0.f;
+    const int tap = kk / p.Ktap;
+    const int c = kk - tap * p.Ktap;
+    const AT* A = (const AT*)p.A;
+    return to_f32(A[(int64_t)(srow + tap * p.dil) * p.lda + c]);
+}
+
+// NE consecutive A elements of row `srow` starting at k index kk0 (NE % 2 == 0), as f32.
+template <typename AT, int AMODE, int NE>
+__device__ __forceinline__ void load_a_run(const ConvGemmParams& p, int srow, int kk0, bool valid,
+                                           float (&v)[NE]) {
+    if (!valid) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[e] = 0.f;
+        return;
+    }
+    if constexpr (AMODE == A_PAIRS) {
+        const float* row = (const float*)p.A + (int64_t)srow * p.lda;
+#pragma unroll
+        for (int e = 0; e < NE; e += 2) {
+            const int kk = kk0 + e;
+            if (kk < p.K) {
+                const float2 t = *(const float2*)(row + kk);
+                v[e] = t.x;
+                v[e + 1] = t.y;
+            } else {
+                v[e] = v[e + 1] = 0.f;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[e] = load_a_scalar<AT>(p, srow, kk0 + e);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Epilogues
+// ---------------------------------------------------------------------------
+// Scalar epilogue (any N): straight from the MFMA accumulator layout.
+template <typename OT>
+__device__ __forceinline__ void epi_store(const ConvGemmParams& p, int m, int n, float v,
+                                          float sc, float sh) {
+    // BatchNorm eval as ATen's CPU kernel evaluates it: x * alpha + beta, two roundings
+    v = __fadd_rn(__fmul_rn(v, sc), sh);
+    if (p.relu) v = v > 0.f ? v : 0.f;
+    if (p.R) v += to_f32(((const OT*)p.R)[(int64_t)res_row(p, m) * p.ldr + n]);
+    ((OT*)p.Y)[(int64_t)m * p.ldy + n] = from_f32<OT>(v);
+}
+
+template <typename OT, int MI>
+__device__ __forceinline__ void epilogue_scalar(const ConvGemmParams& p, const f32x4 (&acc)[MI][4],
+                                                int mw, int nw, int lane) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = nw + j * 16 + (lane & 15);
+        if (n >= p.N) continue;
+        const float sc = p.scale[n], sh = p.shift[n];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = mw + i * 16 + (lane >> 4) * 4 + r;
+                if (m < p.M) epi_store<OT>(p, m, n, acc[i][j][r], sc, sh);
+            }
+    }
+}
+
+// Vector epilogue (N % 8 == 0): each wave transposes its (16*MI)x64 f32 accumulator
+// tile through its own LDS region (row pitch 68 floats: conflict-free writes),
+// then every lane owns 8 consecutive columns of a row: 16/32-byte residual loads
+// and output stores, whole 128-byte lines per 8 lanes.
+constexpr int kEpiLd = 68;
+
+template <typename OT, int MI, int PASS_ROWS>
+__device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x4 (&acc)[MI][4],
+                                             float* stage, int mw, int nw, int lane) {
+    const int c8 = lane & 7;
+    const int n = nw + c8 * 8;
+    const bool nval = n < p.N;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sc[e] = nval ? p.scale[n + e] : 0.f;
+        sh[e] = nval ? p.shift[n + e] : 0.f;
+    }
+#pragma unroll
+    for (int pass = 0; pass < MI * 16 / PASS_ROWS; ++pass) {
+#pragma unroll
+        for (int ii = 0; ii < PASS_ROWS / 16; ++ii) {
+            const int i = pass * (PASS_ROWS / 16) + ii;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    stage[(ii * 16 + (lane >> 4) * 4 + r) * kEpiLd + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PASS_ROWS / 8; ++q) {
+            const int row = q * 8 + (lane >> 3);
+            const int m = mw + pass * PASS_ROWS + row;
+            const f32x4 lo = *(const f32x4*)&stage[row * kEpiLd + c8 * 8];
+            const f32x4 hi = *(const f32x4*)&stage[row * kEpiLd + c8 * 8 + 4];
+            if (m < p.M && nval) {
+                float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    v[e] = __fadd_rn(__fmul_rn(v[e], sc[e]), sh[e]);
+                    if (p.relu) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                }
+                if (p.R) {
+                    const int64_t ro = (int64_t)res_row(p, m) * p.ldr + n;
+                    if constexpr (sizeof(OT) == 2) {
+                        const u32x4 rv = *(const u32x4*)((const OT*)p.R + ro);
+                        typedef OT ot8 __attribute__((ext_vector_type(8)));
+                        const ot8 r8 = __builtin_bit_cast(ot8, rv);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
+                    } else {
+                        const f32x4 r0 = *(const f32x4*)((const float*)p.R + ro);
+                        const f32x4 r1 = *(const f32x4*)((const float*)p.R + ro + 4);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            v[e] += r0[e];
+                            v[e + 4] += r1[e];
+                        }
+                    }
+                }
+                const int64_t yo = (int64_t)m * p.ldy + n;
+                if constexpr (sizeof(OT) == 2) {
+                    typedef OT ot8 __attribute__((ext_vector_type(8)));
+                    ot8 o;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] = (OT)v[e];
+                    *(u32x4*)((OT*)p.Y + yo) = __builtin_bit_cast(u32x4, o);
+                } else {
+                    *(f32x4*)((float*)p.Y + yo) = f32x4{v[0], v[1], v[2], v[3]};
+                    *(f32x4*)((float*)p.Y + yo + 4) = f32x4{v[4], v[5], v[6], v[7]};
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace gemm
+}  // namespace vp3d

@@ -43,8 +43,13 @@ enum class Act { F32 = 0, BF16 = 1, F16 = 2 };
 hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, Act compute,
                             hipStream_t stream);
 
-// Tile geometry the packer must pad to.
-constexpr int kPadN = 128;
+// 256x256 LDS-DMA family (conv_gemm_big.hip) for the large tap-aligned layers.
+bool conv_gemm_big_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
+hipError_t launch_conv_gemm_big(const ConvGemmParams& p, Act out_type, Act compute,
+                                hipStream_t stream);
+
+// Tile geometry the packer must pad to (rows of W to kPadN, K to kPadK).
+constexpr int kPadN = 256;
 constexpr int kPadK = 64;
 
 // preprocess kernels (preprocess.hip)
@@ -58,6 +63,8 @@ hipError_t launch_gather_windows(const float* kps, int f2, const float* cams,
                                  const int64_t* seq_off, const int32_t* seq_len,
                                  const int32_t* pairs, int B, int window, int pad, int shift,
                                  float* out, hipStream_t s);
+hipError_t launch_pack_rows(const float* x, int M, int T_out, int T_in, int stride, int lda,
+                            int K, int Kp, void* out, bool bf16, hipStream_t s);
 hipError_t launch_mpjpe_accumulate(const float* pred, const float* target, int64_t n,
                                    double* acc, hipStream_t s);
 

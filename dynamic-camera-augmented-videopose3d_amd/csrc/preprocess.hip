@@ -8,11 +8,15 @@
 //                      common/models/CamTransformer.py:187-190
 //   mpjpe_accumulate   reference common/loss.py:11-17
 //
-// None of these contract multiply-adds: the reference evaluates them with
-// separately rounded numpy / torch-CPU operations, and the kernels reproduce that
-// rounding sequence (explicit _rn intrinsics) so integer-exact parity holds where
-// the reference's own arithmetic is order-independent.
+// Floating-point contraction is OFF in this file: HIP compiles with
+// -ffp-contract=fast by default and __fadd_rn/__fmul_rn are plain operators, so a
+// mul followed by an add would silently become an FMA.  The reference evaluates
+// these formulas as separately rounded numpy / torch-CPU operations; the kernels
+// spell out exactly that rounding sequence (and use __builtin_fmaf only where
+// torch's own CPU kernel fuses), which makes them bit-exact on the goldens.
 #include "kernels.h"
+
+#pragma clang fp contract(off)
 
 namespace vp3d {
 namespace {
@@ -86,14 +90,15 @@ __global__ void world_to_camera_kernel(const float* __restrict__ X, int64_t n, f
         const float vx = __fsub_rn(X[3 * i + 0], tx);
         const float vy = __fsub_rn(X[3 * i + 1], ty);
         const float vz = __fsub_rn(X[3 * i + 2], tz);
-        // uv = cross(qvec, v)
-        const float uvx = __fsub_rn(__fmul_rn(qy, vz), __fmul_rn(qz, vy));
-        const float uvy = __fsub_rn(__fmul_rn(qz, vx), __fmul_rn(qx, vz));
-        const float uvz = __fsub_rn(__fmul_rn(qx, vy), __fmul_rn(qy, vx));
-        // uuv = cross(qvec, uv)
-        const float uuvx = __fsub_rn(__fmul_rn(qy, uvz), __fmul_rn(qz, uvy));
-        const float uuvy = __fsub_rn(__fmul_rn(qz, uvx), __fmul_rn(qx, uvz));
-        const float uuvz = __fsub_rn(__fmul_rn(qx, uvy), __fmul_rn(qy, uvx));
+        // uv = cross(qvec, v), uuv = cross(qvec, uv): torch-CPU's cross kernel
+        // evaluates each component as fma(a1, b2, -(a2 * b1)) (reproduced bit for
+        // bit on the golden vectors), the rest are separately rounded tensor ops.
+        const float uvx = __builtin_fmaf(qy, vz, -__fmul_rn(qz, vy));
+        const float uvy = __builtin_fmaf(qz, vx, -__fmul_rn(qx, vz));
+        const float uvz = __builtin_fmaf(qx, vy, -__fmul_rn(qy, vx));
+        const float uuvx = __builtin_fmaf(qy, uvz, -__fmul_rn(qz, uvy));
+        const float uuvy = __builtin_fmaf(qz, uvx, -__fmul_rn(qx, uvz));
+        const float uuvz = __builtin_fmaf(qx, uvy, -__fmul_rn(qy, uvx));
         out[3 * i + 0] = __fadd_rn(vx, __fmul_rn(2.f, __fadd_rn(__fmul_rn(qw, uvx), uuvx)));
         out[3 * i + 1] = __fadd_rn(vy, __fmul_rn(2.f, __fadd_rn(__fmul_rn(qw, uvy), uuvy)));
         out[3 * i + 2] = __fadd_rn(vz, __fmul_rn(2.f, __fadd_rn(__fmul_rn(qw, uvz), uuvz)));
@@ -192,6 +197,50 @@ hipError_t launch_mpjpe_accumulate(const float* pred, const float* target, int64
                                    double* acc, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(mpjpe_kernel, grid_for(n, 8), dim3(kThreads), 0, s, pred, target, n, acc);
+    return hipGetLastError();
+}
+
+}  // namespace vp3d
+
+namespace vp3d {
+namespace {
+
+// Row packer for the first (expand) convolution on the 16-bit path: the
+// channel-last f32 input rows that one output frame reads (w0 consecutive frames
+// of J*F values, TemporalModel.py:102/168) become one zero-padded 16-bit GEMM row
+// of Kp elements, so that layer runs on the tap-aligned LDS-DMA kernel.
+template <typename CT>
+__global__ void pack_rows_kernel(const float* __restrict__ x, int M, int T_out, int T_in,
+                                 int stride, int lda, int K, int Kp, CT* __restrict__ out) {
+    const int chunks = Kp >> 3;
+    const int64_t total = (int64_t)M * chunks;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int m = (int)(i / chunks);
+        const int c = (int)(i - (int64_t)m * chunks) * 8;
+        const int b = m / T_out;
+        const int t = m - b * T_out;
+        const float* row = x + ((int64_t)b * T_in + (int64_t)t * stride) * lda;
+        typedef CT ct8 __attribute__((ext_vector_type(8)));
+        ct8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (CT)(c + e < K ? row[c + e] : 0.f);
+        *(ct8*)(out + (int64_t)m * Kp + c) = v;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_pack_rows(const float* x, int M, int T_out, int T_in, int stride, int lda,
+                            int K, int Kp, void* out, bool bf16, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    const dim3 grid = grid_for((int64_t)M * (Kp / 8), 4);
+    if (bf16)
+        hipLaunchKernelGGL(pack_rows_kernel<__bf16>, grid, dim3(kThreads), 0, s, x, M, T_out, T_in,
+                           stride, lda, K, Kp, (__bf16*)out);
+    else
+        hipLaunchKernelGGL(pack_rows_kernel<_Float16>, grid, dim3(kThreads), 0, s, x, M, T_out, T_in,
+                           stride, lda, K, Kp, (_Float16*)out);
     return hipGetLastError();
 }
 

@@ -307,7 +307,9 @@ int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
     std::vector<int> len;
     if (!layer_lengths(h, T, len)) return fail(VP3D_ERR_ARG, "input too short for the receptive field");
     const size_t rows = (size_t)B * len[0];
-    const size_t need = 3 * rows * h->cfg.channels * esize(dtype);
+    // three rotating activation buffers + (16-bit path) the packed expand-conv rows
+    const size_t need = 3 * rows * h->cfg.channels * esize(dtype) +
+                        (dtype == VP3D_DTYPE_F32 ? 0 : rows * h->layers[0].Kp * 2);
     if (need <= h->ws_bytes) return VP3D_OK;
     if (h->ws) HIP_TRY(hipFree(h->ws));
     h->ws = nullptr;
@@ -497,9 +499,7 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
             p.R_off = L.res_off;
             p.ldr = L.cout;
         }
-        const Act a_type = first ? Act::F32 : act;
-        const Act o_type = last ? Act::F32 : act;
-
+        // algorithmic FLOP of the layer (unpadded K), timed from before any packing
         ProfEvent pe{};
         if (h->profiling) {
             pe.layer = li;
@@ -508,6 +508,25 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
             pe.flop = 2.0 * (double)p.M * (double)p.N * (double)p.K;
             hipEventRecord(pe.a, s);
         }
+        Act a_type = first ? Act::F32 : act;
+        if (first && act != Act::F32) {
+            // 16-bit path: pack the f32 input rows of the expand conv into zero-padded
+            // 16-bit GEMM rows (one launch) so the conv runs on the tap-aligned kernel
+            void* packed = base + 3 * buf_elems * es;
+            hipError_t pe = launch_pack_rows((const float*)x, p.M, p.T_out, p.T_in, p.stride, p.lda,
+                                             p.K, p.Kp, packed, act == Act::BF16, s);
+            if (pe != hipSuccess) return fail(VP3D_ERR_HIP, std::string("pack: ") + hipGetErrorString(pe));
+            p.A = packed;
+            p.K = p.Kp;
+            p.Ktap = p.Kp;
+            p.lda = p.Kp;
+            p.T_in = p.T_out;
+            p.stride = 1;
+            p.dil = 1;
+            a_type = act;
+        }
+        const Act o_type = last ? Act::F32 : act;
+
         hipError_t e = launch_conv_gemm(p, a_type, o_type, act, s);
         if (e != hipSuccess)
             return fail(VP3D_ERR_HIP, std::string("conv layer ") + std::to_string(li) + ": " +
@@ -520,9 +539,6 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
         if (!last && !L.residual && !first) {
             block_in = cur_in;
             block_len = cur_len;
-        }
-        if (first) {
-            // expand output is the first block's input
         }
         cur_in = p.Y;
         cur_len = len[li];
