@@ -22,6 +22,9 @@
 //     each lane's SOURCE address (its inverse permutation), never to the LDS side;
 //   * the workgroup -> tile map is XCD-aware (consecutive tiles on one XCD share
 //     the A panel in that XCD's L2).
+#include <cstdlib>
+#include <cstring>
+
 #include "gemm_common.h"
 
 namespace vp3d {
@@ -33,20 +36,30 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 constexpr int BM2 = 256;
-constexpr int BN2 = 256;
 constexpr int BK2 = 32;
-constexpr int NSLOT = 4;
-constexpr int SLOT_BYTES = (BM2 + BN2) * BK2 * 2;  // 32 KB: A rows then B rows
-constexpr int RING_BYTES = NSLOT * SLOT_BYTES;     // 128 KB
-constexpr int EPI_BYTES = 8 * 32 * kEpiLd * 4;     // 8 waves x 32-row passes
-constexpr int SMEM2 = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
 
-__device__ __forceinline__ void wait_vm(int n_after) {
-    // outstanding LDS-DMA of this wave allowed to remain in flight (4 per K-step)
-    if (n_after >= 2)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n_after == 1)
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+template <int NW_N, int NSLOT>
+struct BigCfg {
+    static constexpr int BN = 64 * NW_N;                 // 256 (8 waves) or 128 (4 waves)
+    static constexpr int NWAVES = 2 * NW_N;
+    static constexpr int THREADS = 64 * NWAVES;
+    static constexpr int A_PIECES = (BM2 / 16) / NWAVES;  // 1 KB LDS-DMA pieces per wave per K-step
+    static constexpr int B_PIECES = (BN / 16) / NWAVES;
+    static constexpr int DMA_PER_STEP = A_PIECES + B_PIECES;
+    static constexpr int SLOT_BYTES = (BM2 + BN) * BK2 * 2;
+    static constexpr int RING_BYTES = NSLOT * SLOT_BYTES;
+    static constexpr int EPI_BYTES = NWAVES * 32 * kEpiLd * 4;
+    static constexpr int SMEM = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
+};
+
+// Counted wait: this wave's LDS-DMA of the current K-step has landed while `after`
+// later K-steps (DMA_PER_STEP instructions each) stay in flight.
+template <int PER_STEP>
+__device__ __forceinline__ void wait_vm(int after) {
+    if (after >= 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_STEP) : "memory");
+    else if (after == 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STEP) : "memory");
     else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -56,37 +69,43 @@ __device__ __forceinline__ void block_sync_lds() {
     asm volatile("" ::: "memory");
 }
 
-template <typename CT, typename OT>
-__global__ __launch_bounds__(512, 2) void conv_gemm_h16_256(ConvGemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+// PIPE: fragments of K-step s+1 are read from LDS into a second register set
+//       while the MFMAs of step s run (the ds_read latency leaves the critical path);
+// PRIO: s_setprio(1) around each MFMA cluster (cdna_hip_programming.md §5.5 T5).
+template <typename CT, typename OT, int NW_N, int NSLOT, bool PIPE, bool PRIO>
+__global__ __launch_bounds__(128 * NW_N, 2) void conv_gemm_h16_big(ConvGemmParams p) {
+    using C = BigCfg<NW_N, NSLOT>;
+    __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
-    const int wr = wid >> 2, wc = wid & 3;
+    const int wr = wid / NW_N, wc = wid % NW_N;
 
-    const int ntn = (p.N + BN2 - 1) / BN2;
+    const int ntn = (p.N + C::BN - 1) / C::BN;
     const int ntm = (p.M + BM2 - 1) / BM2;
     const int wg = xcd_remap(blockIdx.x, ntm * ntn);
     const int tile_m = wg / ntn;
     const int tile_n = wg - tile_m * ntn;
-    const int m0 = tile_m * BM2, n0 = tile_n * BN2;
+    const int m0 = tile_m * BM2, n0 = tile_n * C::BN;
 
     // ---- LDS-DMA source addressing (per lane, fixed for the whole K loop) ----
-    // A wave issues pieces {wid, wid+8} of A and of B per K-step; piece pc covers
-    // rows pc*16 .. pc*16+15 (1 KB).  Lane l fills LDS chunk (l & 3) of row
-    // pc*16 + (l >> 2); that physical chunk holds logical chunk c:
+    // Piece pc of an operand covers rows pc*16 .. pc*16+15 (1 KB); wave w issues
+    // pieces w, w + NWAVES, ...  Lane l fills LDS chunk (l & 3) of row
+    // pc*16 + (l >> 2); that physical chunk holds logical chunk dma_c:
     const int dma_row = lane >> 2;
     const int dma_c = ((lane & 3) - 2 * ((lane >> 4) & 3)) & 3;
-    int a_src[2];
-    int64_t b_off[2];
+    int a_src[C::A_PIECES];
+    int64_t b_off[C::B_PIECES];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int pc = wid + 8 * q;
-        int m = m0 + pc * 16 + dma_row;
+    for (int q = 0; q < C::A_PIECES; ++q) {
+        int m = m0 + (wid + C::NWAVES * q) * 16 + dma_row;
         m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; their outputs are never stored
         a_src[q] = src_row(p, m);
-        const int n = n0 + pc * 16 + dma_row;  // W is padded to a multiple of 256 rows
+    }
+#pragma unroll
+    for (int q = 0; q < C::B_PIECES; ++q) {
+        const int n = n0 + (wid + C::NWAVES * q) * 16 + dma_row;  // W rows padded to 256
         b_off[q] = (int64_t)n * p.Kp + dma_c * 8;
     }
     const CT* A = (const CT*)p.A;
@@ -96,20 +115,23 @@ __global__ __launch_bounds__(512, 2) void conv_gemm_h16_256(ConvGemmParams p) {
         const int k0 = s * BK2;
         const int tap = k0 / p.Ktap;
         const int cin = k0 - tap * p.Ktap + dma_c * 8;
-        char* slot = smem + (s % NSLOT) * SLOT_BYTES;
+        char* slot = smem + (s % NSLOT) * C::SLOT_BYTES;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int pc = wid + 8 * q;
+        for (int q = 0; q < C::A_PIECES; ++q) {
             const CT* ga = A + (int64_t)(a_src[q] + tap * p.dil) * p.lda + cin;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)ga, (lds_ptr_t)(slot + pc * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)ga,
+                                             (lds_ptr_t)(slot + (wid + C::NWAVES * q) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < C::B_PIECES; ++q) {
             const CT* gb = W + b_off[q] + k0;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)gb,
-                                             (lds_ptr_t)(slot + BM2 * BK2 * 2 + pc * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(
+                (gbl_ptr_t)gb, (lds_ptr_t)(slot + BM2 * BK2 * 2 + (wid + C::NWAVES * q) * 1024), 16, 0, 0);
         }
     };
 
-    // ---- fragment read addressing: row (l & 15) of each 16-row block, logical
-    // chunk (l >> 4) -> physical chunk (c + 2*((r>>2)&3)) & 3 (lane-constant) ----
+    // ---- fragment reads: row (l & 15) of each 16-row block, logical chunk (l >> 4)
+    // -> physical chunk (c + 2*((r>>2)&3)) & 3, lane-constant ----
     const int frag_chunk = ((lane >> 4) + 2 * (((lane & 15) >> 2) & 3)) & 3;
     const int a_frag_off = (wr * 128 + (lane & 15)) * 64 + frag_chunk * 16;
     const int b_frag_off = BM2 * BK2 * 2 + (wc * 64 + (lane & 15)) * 64 + frag_chunk * 16;
@@ -120,24 +142,60 @@ __global__ __launch_bounds__(512, 2) void conv_gemm_h16_256(ConvGemmParams p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    struct Frag {
+        u32x4 a[8];
+        u32x4 b[4];
+    };
+    auto read_frags = [&](int s, Frag& f) {
+        const char* slot = smem + (s % NSLOT) * C::SLOT_BYTES;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f.b[j] = *(const u32x4*)(slot + b_frag_off + j * 16 * 64);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f.a[i] = *(const u32x4*)(slot + a_frag_off + i * 16 * 64);
+    };
+    auto mma = [&](const Frag& f) {
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<CT>(f.a[i], f.b[j], acc[i][j]);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    };
+
     const int nk = p.Kp / BK2;
     const int pre = nk < NSLOT - 1 ? nk : NSLOT - 1;
     for (int s = 0; s < pre; ++s) issue(s);
 
-    for (int s = 0; s < nk; ++s) {
-        const int left = nk - 1 - s;  // K-steps after s already issued (capped at 2)
-        wait_vm(left < 2 ? left : 2);
-        block_sync_lds();  // slot s landed for every wave; slot s-1 fully consumed
-        if (s + NSLOT - 1 < nk) issue(s + NSLOT - 1);
-        const char* slot = smem + (s % NSLOT) * SLOT_BYTES;
-        u32x4 bfr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = *(const u32x4*)(slot + b_frag_off + j * 16 * 64);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const u32x4 afr = *(const u32x4*)(slot + a_frag_off + i * 16 * 64);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<CT>(afr, bfr[j], acc[i][j]);
+    if constexpr (!PIPE) {
+        for (int s = 0; s < nk; ++s) {
+            const int left = nk - 1 - s;
+            wait_vm<C::DMA_PER_STEP>(left < NSLOT - 2 ? left : NSLOT - 2);
+            block_sync_lds();  // slot s landed for every wave; slot s-1 fully consumed
+            if (s + NSLOT - 1 < nk) issue(s + NSLOT - 1);
+            Frag f;
+            read_frags(s, f);
+            mma(f);
+        }
+    } else {
+        // stage s+1 must be resident one step early; slot s-1 (read during step s-2,
+        // consumed by step s-1) is the one refilled at step s
+        wait_vm<C::DMA_PER_STEP>(pre - 1);
+        block_sync_lds();
+        Frag f0, f1;
+        read_frags(0, f0);
+        auto step = [&](int s, Frag& cur, Frag& nxt) {
+            if (s + 1 < nk) {
+                const int issued = nk < s + NSLOT - 1 ? nk : s + NSLOT - 1;
+                wait_vm<C::DMA_PER_STEP>(issued - (s + 2));
+                block_sync_lds();
+                if (s + NSLOT - 1 < nk) issue(s + NSLOT - 1);
+                read_frags(s + 1, nxt);
+            }
+            mma(cur);
+        };
+        for (int s = 0; s < nk; s += 2) {
+            step(s, f0, f1);
+            if (s + 1 < nk) step(s + 1, f1, f0);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -145,6 +203,30 @@ __global__ __launch_bounds__(512, 2) void conv_gemm_h16_256(ConvGemmParams p) {
 
     const int mw = m0 + wr * 128, nw = n0 + wc * 64;
     epilogue_vec<OT, 8, 32>(p, acc, (float*)smem + wid * 32 * kEpiLd, mw, nw, lane);
+}
+
+// Tile shape choice (VP3D_BIG_TILE=256|128 overrides, for A/B runs):
+//   256x256, 8 waves, 4-slot ring (128 KB LDS): one workgroup per CU, least L2 traffic
+//   256x128, 4 waves, 3-slot ring (72 KB LDS): two workgroups per CU, so one
+//   workgroup's prologue/epilogue overlaps the other's MFMA main loop
+// Main-loop variant (VP3D_BIG_VARIANT=plain|pipe|pipe_prio, default pipe).
+int big_variant() {
+    static int v = [] {
+        const char* e = getenv("VP3D_BIG_VARIANT");
+        if (!e) return 1;
+        if (!strcmp(e, "plain")) return 0;
+        if (!strcmp(e, "pipe_prio")) return 2;
+        return 1;
+    }();
+    return v;
+}
+
+int big_tile_n() {
+    static int v = [] {
+        const char* e = getenv("VP3D_BIG_TILE");
+        return (e && atoi(e) == 256) ? 256 : 128;
+    }();
+    return v;
 }
 
 }  // namespace
@@ -157,26 +239,45 @@ bool conv_gemm_big_eligible(const ConvGemmParams& p, Act a_type, Act out_type, A
     if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
         (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
         return false;
-    // enough tiles to fill the 256 CUs about four times over
-    const int64_t tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + BN2 - 1) / BN2);
-    return tiles >= 4 * 256;
+    // enough tiles to fill the 256 CUs several times over
+    const int bn = big_tile_n();
+    const int64_t tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + bn - 1) / bn);
+    return tiles >= (bn == 256 ? 4 : 8) * 256;
+}
+
+template <typename CT, typename OT, int NW_N, int NSLOT>
+void launch_big_v(const ConvGemmParams& p, dim3 grid, hipStream_t stream) {
+    switch (big_variant()) {
+        case 0:
+            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, false, false>), grid,
+                               dim3(128 * NW_N), 0, stream, p);
+            break;
+        case 2:
+            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, true, true>), grid,
+                               dim3(128 * NW_N), 0, stream, p);
+            break;
+        default:
+            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, true, false>), grid,
+                               dim3(128 * NW_N), 0, stream, p);
+    }
+}
+
+template <typename CT, typename OT>
+hipError_t launch_big_t(const ConvGemmParams& p, hipStream_t stream) {
+    if (big_tile_n() == 256)
+        launch_big_v<CT, OT, 4, 4>(p, dim3(((p.M + BM2 - 1) / BM2) * ((p.N + 255) / 256)), stream);
+    else
+        launch_big_v<CT, OT, 2, 3>(p, dim3(((p.M + BM2 - 1) / BM2) * ((p.N + 127) / 128)), stream);
+    return hipGetLastError();
 }
 
 hipError_t launch_conv_gemm_big(const ConvGemmParams& p, Act out_type, Act compute,
                                 hipStream_t stream) {
-    const dim3 grid(((p.M + BM2 - 1) / BM2) * ((p.N + BN2 - 1) / BN2));
-    if (compute == Act::BF16) {
-        if (out_type == Act::F32)
-            hipLaunchKernelGGL((conv_gemm_h16_256<bf16, float>), grid, dim3(512), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_h16_256<bf16, bf16>), grid, dim3(512), 0, stream, p);
-    } else {
-        if (out_type == Act::F32)
-            hipLaunchKernelGGL((conv_gemm_h16_256<f16, float>), grid, dim3(512), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_h16_256<f16, f16>), grid, dim3(512), 0, stream, p);
-    }
-    return hipGetLastError();
+    if (compute == Act::BF16)
+        return out_type == Act::F32 ? launch_big_t<bf16, float>(p, stream)
+                                    : launch_big_t<bf16, bf16>(p, stream);
+    return out_type == Act::F32 ? launch_big_t<f16, float>(p, stream)
+                                : launch_big_t<f16, f16>(p, stream);
 }
 
 }  // namespace vp3d

@@ -8,9 +8,9 @@
 //                      common/models/CamTransformer.py:187-190
 //   mpjpe_accumulate   reference common/loss.py:11-17
 //
-// Floating-point contraction is OFF in this file: HIP compiles with
-// -ffp-contract=fast by default and __fadd_rn/__fmul_rn are plain operators, so a
-// mul followed by an add would silently become an FMA.  The reference evaluates
+// Floating-point contraction is OFF (build flag -ffp-contract=off, plus the pragma
+// below): HIP compiles with -ffp-contract=fast by default and __fadd_rn/__fmul_rn
+// are plain operators, so a mul followed by an add would silently become an FMA.  The reference evaluates
 // these formulas as separately rounded numpy / torch-CPU operations; the kernels
 // spell out exactly that rounding sequence (and use __builtin_fmaf only where
 // torch's own CPU kernel fuses), which makes them bit-exact on the goldens.

@@ -24,7 +24,10 @@ HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "gemm_common.h"),
 ARCH = os.environ.get("VP3D_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-I", INCLUDE, "-I", CSRC,
+# -ffp-contract=off: HIP defaults to fast contraction, and the HIP headers' __fmul_rn /
+# __fadd_rn carry that flag from their own definition, so a per-file pragma is not
+# enough to keep the reference's separately rounded mul/add sequences intact.
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-I", INCLUDE, "-I", CSRC,
                 "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-value",
                 "-Wno-unused-result"]
 

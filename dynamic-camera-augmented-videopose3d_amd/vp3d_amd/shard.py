@@ -1,0 +1,64 @@
+"""Embarrassingly parallel sharding of the lifter over ranks (one process per GPU).
+
+SURVEY.md §8(e): windows (Optimized1f) are independent, so a global batch of B
+windows is split into contiguous per-rank shards with no data-path collective;
+long sequences (dilated TemporalModel) split by time with a read-only input halo
+of receptive_field - 1 frames per shard (no exchange).  The only collective is
+the end-of-run metric reduction: (sum of per-joint errors, count) — 16 bytes per
+rank — reduced once with all_reduce.
+
+The helpers here are pure index arithmetic plus that single reduction, so they are
+exercised on CPU with the gloo backend (tests/test_shard_gloo.py) and run
+unchanged over RCCL on the GPU node.
+"""
+from __future__ import annotations
+
+from typing import Callable, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [start, end) of `total` items owned by `rank`; sizes differ by <= 1."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def time_shard(T_out: int, rank: int, world: int, receptive_field: int) -> Tuple[int, int, int, int]:
+    """Output frames [o0, o1) of a sequence with T_out outputs owned by `rank`, and the
+    input frames [i0, i1) they need (T_in = T_out + rf - 1; output t reads inputs
+    t .. t + rf - 1).  Neighbouring shards overlap by rf - 1 input frames (the halo)."""
+    o0, o1 = shard_range(T_out, rank, world)
+    return o0, o1, o0, o1 + receptive_field - 1
+
+
+def forward_sharded_windows(fn: Callable[[torch.Tensor], torch.Tensor], windows: torch.Tensor,
+                            rank: int, world: int) -> torch.Tensor:
+    """Run `fn` on this rank's contiguous shard of a (B, T, J, F) window batch."""
+    s, e = shard_range(int(windows.shape[0]), rank, world)
+    return fn(windows[s:e])
+
+
+def forward_sharded_sequence(fn: Callable[[torch.Tensor], torch.Tensor], seq: torch.Tensor,
+                             receptive_field: int, rank: int, world: int) -> torch.Tensor:
+    """Run a dilated-model `fn` on this rank's time shard of a padded (1, T_in, J, F)
+    sequence; returns the (1, o1 - o0, J_out, 3) slice of the full output."""
+    T_out = int(seq.shape[1]) - receptive_field + 1
+    o0, o1, i0, i1 = time_shard(T_out, rank, world, receptive_field)
+    if o1 <= o0:
+        return seq.new_zeros((1, 0) + tuple(seq.shape[2:3]) + (3,))
+    return fn(seq[:, i0:i1])
+
+
+def reduce_mpjpe(err_sum: float, count: float, device=None) -> float:
+    """Global MPJPE from per-rank (sum of errors, count) with one all_reduce
+    (identity when torch.distributed is not initialised)."""
+    t = torch.tensor([float(err_sum), float(count)], dtype=torch.float64,
+                     device=device if device is not None else "cpu")
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t[0] / t[1]) if t[1] > 0 else float("nan")

@@ -1,0 +1,78 @@
+"""Multi-rank sharding rehearsed on CPU with the gloo backend,
+world_size 2: window shards and halo'd time shards reassemble the unsharded
+output exactly, and the single end-of-run all_reduce gives the global MPJPE.
+The per-shard compute here is the CPU oracle (test infrastructure); on the GPU
+node the same shard arithmetic feeds libvp3d (bench.py under torchrun)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from vp3d_amd import shard, synth
+
+FW = [3, 3, 3]
+RF = 27
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _state():
+    from common.models.TemporalModel import TemporalModel
+    m = TemporalModel(17, 2, 17, FW, channels=32)
+    return synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in m.state_dict().items()], seed=5)
+
+
+def _worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle.temporal_ref import lifter_forward
+    sd = _state()
+    win = torch.from_numpy(synth.normalized_windows(6, "shardwin", 11, RF))
+    y_w = shard.forward_sharded_windows(lambda x: lifter_forward(sd, x, FW, strided=True), win, rank, world)
+    seq = torch.from_numpy(synth.normalized_windows(6, "shardseq", 1, 200))
+    y_s = shard.forward_sharded_sequence(lambda x: lifter_forward(sd, x, FW), seq, RF, rank, world)
+    gt = torch.from_numpy(synth.gt_poses(3, "shardgt", 11, 17)).view(11, 1, 17, 3)
+    s, e = shard.shard_range(11, rank, world)
+    err = torch.linalg.norm(y_w - gt[s:e], dim=-1)
+    g = shard.reduce_mpjpe(float(err.sum()), float(err.numel()))
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), y_w=y_w.numpy(), y_s=y_s.numpy(), g=g)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_ranges():
+    assert [shard.shard_range(10, r, 3) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
+    assert [shard.shard_range(2, r, 4) for r in range(4)] == [(0, 1), (1, 2), (2, 2), (2, 2)]
+    o0, o1, i0, i1 = shard.time_shard(100, 1, 2, 243)
+    assert (o0, o1, i0, i1) == (50, 100, 50, 342)
+    with pytest.raises(ValueError):
+        shard.shard_range(10, 2, 2)
+
+
+def test_gloo_world2(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    from oracle.temporal_ref import lifter_forward
+    sd = _state()
+    win = torch.from_numpy(synth.normalized_windows(6, "shardwin", 11, RF))
+    y_full = lifter_forward(sd, win, FW, strided=True).numpy()
+    seq = torch.from_numpy(synth.normalized_windows(6, "shardseq", 1, 200))
+    ys_full = lifter_forward(sd, seq, FW).numpy()
+    parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
+    assert np.array_equal(np.concatenate([p["y_w"] for p in parts]), y_full)
+    assert np.allclose(np.concatenate([p["y_s"] for p in parts], axis=1), ys_full, atol=1e-6)
+    gt = synth.gt_poses(3, "shardgt", 11, 17).reshape(11, 1, 17, 3)
+    want = float(np.mean(np.linalg.norm(y_full.astype(np.float64) - gt, axis=-1)))
+    for p in parts:
+        assert abs(float(p["g"]) - want) < 1e-6
