@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--traj", action="store_true",
                     help="config 3: camera-trajectory conditioned input (46 ch) with the "
                          "on-device window gather inside the timed step")
+    ap.add_argument("--stream", action="store_true",
+                    help="config 5: causal streaming, one frame per step, hipGraph replay "
+                         "(use --dtype fp16 and a large --steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="approximate CPU-baseline sample duration (0 disables)")
     ap.add_argument("--parity-windows", type=int, default=32)
@@ -64,6 +67,108 @@ def synth_windows(B, T, jin, seed, device):
     return (base + torch.cumsum(steps, dim=1)).contiguous()
 
 
+def stream_main(args, world, rank, dev):
+    """Config 5: causal TemporalModel, one frame in / one pose out per step, the
+    10-kernel step replayed from a hipGraph; HBM-bound weight streaming."""
+    from common.models.TemporalModel import TemporalModel
+    from oracle.temporal_ref import lifter_forward
+    from vp3d_amd import synth
+    from vp3d_amd.stream import CausalStream
+
+    model = TemporalModel(JOINTS, 2, JOINTS, FW, causal=True, channels=CHANNELS)
+    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.eval().cuda()
+    st = CausalStream(model.native_lifter(dev), args.dtype)
+    s = torch.cuda.Stream(dev)
+    fin, fout = st.io_tensors()
+    st.capture(s)
+    frames = synth_windows(1, max(args.steps, 1) + args.warmup, JOINTS, 1000 + rank, dev)[0]
+    frames = frames.reshape(frames.shape[0], -1)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):
+        for t in range(args.warmup):
+            fin.copy_(frames[t])
+            st.replay(s)
+        s.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(s)
+        for t in range(args.steps):
+            fin.copy_(frames[args.warmup + t])
+            st.replay(s)
+        ev1.record(s)
+        s.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        return
+    # algorithmic bytes per step: every weight of the stack once (unpadded), step dtype
+    wbytes = {"fp32": 4, "bf16": 2, "fp16": 2}[args.dtype]
+    n_w = sum(v.size for k, v in sd.items() if (k.startswith("layers_conv") or k.startswith("expand_conv")
+                                                 or k == "shrink.weight") and k.endswith("weight"))
+    step_bytes = n_w * wbytes
+    step_s = ev_ms * 1e-3 / args.steps
+    achieved = step_bytes / step_s / 1e9
+    # parity: first 64 frames of a stream vs the whole-sequence causal evaluation
+    T = 64
+    xs = synth_windows(1, T, JOINTS, 7, dev)
+    st.reset()
+    outs = torch.stack([st.step(xs[0, t]).clone() for t in range(T)]).cpu().numpy()
+    pad = (RF_FULL - 1) // 2
+    xp = torch.cat([xs[:, :1].expand(1, 2 * pad, -1, -1), xs], dim=1).cpu()
+    ref = lifter_forward(sd, xp, FW, causal=True).numpy()[0]
+    gt = synth.gt_poses(3, "stream_gt", T, JOINTS)
+
+    def mp(a):
+        return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
+    cpu = None
+    if args.cpu_seconds > 0:
+        win = xp[:, :RF_FULL].contiguous()
+        lifter_forward(sd, win, FW, causal=True)
+        n, tc = 0, 0.0
+        while tc < args.cpu_seconds:
+            t1 = time.perf_counter()
+            lifter_forward(sd, win, FW, causal=True)
+            tc += time.perf_counter() - t1
+            n += 1
+        cpu = {"value": round(n / tc, 2), "unit": "poses/s", "cores": torch.get_num_threads(),
+               "kind": "port", "sample": f"{n} single-frame causal steps (one 243-frame window "
+                                         f"through the torch-CPU restatement each) in {tc:.1f} s"}
+    out = {
+        "metric": METRIC, "value": round(world * args.steps / dt, 2), "unit": "poses/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (seeded random-walk 2D frames, counter-hash weights)",
+        "config": {"workload": "config5 causal streaming TemporalModel 243-frame RF, 17 joints, "
+                               "1024 ch, one frame per step, hipGraph replay (10 GEMV launches)",
+                   "frames_per_step": 1, "parallelism": f"replicas{world}"},
+        "roofline": {"bound": "hbm", "kernel": "stream step (hipGraph of 10 stream_gemv)",
+                     "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(achieved / 8000.0, 4), "traffic": None,
+                     "bytes_per_step": step_bytes, "avg_step_us": round(step_s * 1e6, 3)},
+        "cpu_baseline": cpu,
+        "parity": {"frames": T, f"{args.dtype}_max_coord_delta_mm": float(np.abs(outs - ref).max()) * 1e3,
+                   f"{args.dtype}_mpjpe_delta_mm": abs(mp(outs) - mp(ref)) * 1e3},
+    }
+    if cpu:
+        out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
+    print(json.dumps(out), flush=True)
+
+
+RF_FULL = 243
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -73,6 +178,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.stream:
+        stream_main(args, world, rank, dev)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     from common.models.TemporalModel import TemporalModelOptimized1f
     from vp3d_amd import synth

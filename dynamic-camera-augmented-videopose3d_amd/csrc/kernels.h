@@ -52,6 +52,25 @@ hipError_t launch_conv_gemm_big(const ConvGemmParams& p, Act out_type, Act compu
 constexpr int kPadN = 256;
 constexpr int kPadK = 64;
 
+// Causal streaming step (stream_step.hip): one GEMV layer per launch.
+struct StreamLayerParams {
+    const void* W;            // packed weights [Np][Kp] of the step dtype
+    const float* scale;       // [N]
+    const float* shift;       // [N]
+    int N, K, Kp, cin, taps, dil, relu;
+    const float* in;          // input ring (in_R slots of cin floats) or plain vector (in_R == 0)
+    int in_R;
+    const float* in_frame;    // expand layer: the new frame (read for tap time == t)
+    float* in_ring_w;         // expand layer: ring slot the new frame is appended to
+    const float* res;         // residual ring (block input) or nullptr
+    int res_R;
+    float* out;               // output ring (out_R slots of N floats) or plain vector
+    int out_R;
+    int* frames_seen;         // device stream position t
+    int advance;              // last layer: single workgroup, t += 1 at the end
+};
+hipError_t launch_stream_gemv(const StreamLayerParams& q, Act wtype, hipStream_t s);
+
 // preprocess kernels (preprocess.hip)
 hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, float* out,
                                    bool inverse, hipStream_t s);

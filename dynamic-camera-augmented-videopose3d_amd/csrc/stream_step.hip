@@ -1,0 +1,149 @@
+// Causal streaming step: one new 2D frame in, one 3D pose out (BASELINE config 5).
+//
+// The causal dilated TemporalModel (reference common/models/TemporalModel.py:79-138
+// with causal=True; causal_shift = pad, so block i's residual is the NEWEST frame
+// of its input, :132) evaluated one frame at a time.  Every convolution becomes a
+// GEMV over the layer's taps, read from per-layer ring buffers of past activations:
+//
+//   layer input x_i (C floats per frame) kept for 2*d_i + 1 frames (ring of R_i = 2^k)
+//   k-conv(t)  = sum_k W_k x_i[t - (w-1-k) d_i]          (TemporalModel.py:134)
+//   x_{i+1}(t) = x_i[t] + relu(bn(W_1x1 relu(bn(k-conv(t)))))  (:135)
+//
+// Stream start: the reference edge-pads a causal sequence with 2*pad copies of
+// frame 0 (generators.py:193-198 with causal_shift = pad).  Every activation whose
+// aligned time is <= 0 therefore equals the one at time 0, so a tap that reaches
+// before the stream start reads time 0 — exact equivalence, no warm-up frames.
+//
+// The stream position lives in device memory (frames_seen), read by every kernel
+// and advanced by the last one, so the whole step is replayable from a hipGraph
+// with fixed kernel arguments.
+//
+// Each kernel is weight-streaming (1 FLOP per weight byte at fp16): the GEMV
+// stages the layer's input vector in LDS and every wave streams whole weight rows
+// with 16-byte loads, several in flight per lane.
+#include "kernels.h"
+
+namespace vp3d {
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kMaxK = 4096;  // per-step input vector (taps * Cin) staged in LDS
+
+template <typename WT>
+__device__ __forceinline__ float wdot8(const u32x4 w, const float* v) {
+    typedef WT wt8 __attribute__((ext_vector_type(8)));
+    const wt8 x = __builtin_bit_cast(wt8, w);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s = __builtin_fmaf((float)x[e], v[e], s);
+    return s;
+}
+
+template <>
+__device__ __forceinline__ float wdot8<float>(const u32x4 w, const float* v) {
+    (void)w;
+    (void)v;
+    return 0.f;  // f32 weights use the 4-wide path below
+}
+
+__device__ __forceinline__ float wave_sum(float s) {
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    return s;
+}
+
+// One streaming GEMV layer.  in: input ring (or plain vector when in_R == 0),
+// optionally the raw input frame for the newest tap of the expand conv.
+template <typename WT>
+__global__ __launch_bounds__(1024) void stream_gemv(StreamLayerParams q) {
+    __shared__ __attribute__((aligned(16))) float v[kMaxK];
+    const int t = *q.frames_seen;
+    const int tid = threadIdx.x;
+
+    // stage the input vector: tap k reads stream time t - (taps-1-k)*dil, clamped at 0
+    for (int kk = tid; kk < q.Kp; kk += blockDim.x) {
+        float val = 0.f;
+        if (kk < q.K) {
+            const int tap = kk / q.cin;
+            const int c = kk - tap * q.cin;
+            int tt = t - (q.taps - 1 - tap) * q.dil;
+            tt = tt < 0 ? 0 : tt;
+            if (q.in_frame && tt == t)
+                val = q.in_frame[c];
+            else if (q.in_R)
+                val = q.in[(int64_t)(tt & (q.in_R - 1)) * q.cin + c];
+            else
+                val = q.in[c];
+        }
+        v[kk] = val;
+    }
+    // the expand layer also appends the new frame to its input ring (slot of time t;
+    // the other taps of this step read older slots, so no workgroup races with it)
+    if (q.in_frame && q.in_ring_w && blockIdx.x == 0)
+        for (int c = tid; c < q.cin; c += blockDim.x)
+            q.in_ring_w[(int64_t)(t & (q.in_R - 1)) * q.cin + c] = q.in_frame[c];
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int nwaves = blockDim.x >> 6;
+    for (int n = blockIdx.x * nwaves + wave; n < q.N; n += gridDim.x * nwaves) {
+        float s = 0.f;
+        if constexpr (sizeof(WT) == 2) {
+            const WT* wr = (const WT*)q.W + (int64_t)n * q.Kp;
+            // 512 elements per wave-iteration: each lane 8 (16 bytes)
+            for (int k0 = 0; k0 < q.Kp; k0 += 512) {
+                const int k = k0 + lane * 8;
+                if (k < q.Kp) s += wdot8<WT>(*(const u32x4*)(wr + k), &v[k]);
+            }
+        } else {
+            const float* wr = (const float*)q.W + (int64_t)n * q.Kp;
+            for (int k0 = 0; k0 < q.Kp; k0 += 256) {
+                const int k = k0 + lane * 4;
+                if (k < q.Kp) {
+                    const float4 w4 = *(const float4*)(wr + k);
+                    s = __builtin_fmaf(w4.x, v[k], s);
+                    s = __builtin_fmaf(w4.y, v[k + 1], s);
+                    s = __builtin_fmaf(w4.z, v[k + 2], s);
+                    s = __builtin_fmaf(w4.w, v[k + 3], s);
+                }
+            }
+        }
+        s = wave_sum(s);
+        if (lane == 0) {
+            float y = s * q.scale[n] + q.shift[n];
+            if (q.relu) y = y > 0.f ? y : 0.f;
+            if (q.res) y += q.res[(int64_t)(q.res_R ? (t & (q.res_R - 1)) : 0) * q.N + n];
+            const int64_t o = q.out_R ? (int64_t)(t & (q.out_R - 1)) * q.N + n : n;
+            q.out[o] = y;
+        }
+    }
+    if (q.advance) {
+        // last layer of the step: one workgroup; advance the stream position after
+        // every wave has read it
+        __syncthreads();
+        if (tid == 0) *q.frames_seen = t + 1;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_stream_gemv(const StreamLayerParams& q, Act wtype, hipStream_t s) {
+    if (q.Kp > kMaxK) return hipErrorInvalidValue;
+    const int nwaves = 4;
+    int grid = (q.N + nwaves - 1) / nwaves;
+    dim3 block(256);
+    if (q.advance) {  // single workgroup of 16 waves
+        grid = 1;
+        block = dim3(1024);
+    }
+    if (wtype == Act::F32)
+        hipLaunchKernelGGL(stream_gemv<float>, dim3(grid), block, 0, s, q);
+    else if (wtype == Act::F16)
+        hipLaunchKernelGGL(stream_gemv<_Float16>, dim3(grid), block, 0, s, q);
+    else
+        hipLaunchKernelGGL(stream_gemv<__bf16>, dim3(grid), block, 0, s, q);
+    return hipGetLastError();
+}
+
+}  // namespace vp3d

@@ -587,6 +587,228 @@ int vp3d_profile_read(vp3d_handle* h, double* ms_total, int64_t* launches, doubl
     return VP3D_OK;
 }
 
+// ---- causal streaming ----
+
+}  // extern "C"
+
+struct vp3d_stream {
+    vp3d_handle* h = nullptr;
+    int dtype = VP3D_DTYPE_F16;
+    int* frames_seen = nullptr;        // device
+    float* in_frame = nullptr;         // device, J_in*F
+    float* out_pose = nullptr;         // device, J_out*3
+    float* rings = nullptr;            // all ring buffers
+    float* scratch = nullptr;          // k-conv output, last block output
+    std::vector<StreamLayerParams> steps;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+namespace {
+
+int pow2_at_least(int v) {
+    int r = 1;
+    while (r < v) r <<= 1;
+    return r;
+}
+
+int stream_launch(vp3d_stream* st, hipStream_t s) {
+    const Act wt = st->dtype == VP3D_DTYPE_F32 ? Act::F32 : (st->dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16);
+    for (const StreamLayerParams& q : st->steps) HIP_TRY(launch_stream_gemv(q, wt, s));
+    return VP3D_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
+    if (!h || !out) return fail(VP3D_ERR_ARG, "NULL argument");
+    *out = nullptr;
+    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    if (h->cfg.variant != VP3D_VARIANT_DILATED || !h->cfg.causal)
+        return fail(VP3D_ERR_ARG, "streaming needs a causal dilated TemporalModel");
+    for (const Layer& L : h->layers)
+        if (L.Kp > 4096) return fail(VP3D_ERR_ARG, "streaming supports K <= 4096 per layer");
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev != h->device) return fail(VP3D_ERR_STATE, "handle belongs to another device");
+
+    vp3d_stream* st = new vp3d_stream();
+    st->h = h;
+    st->dtype = dtype;
+    const int C = h->cfg.channels;
+    const int nl = (int)h->layers.size();
+    const int nb = h->cfg.n_widths - 1;
+    // ring i holds the input of layer (expand: raw frames) / block i
+    std::vector<int> ring_len, ring_width;
+    ring_len.push_back(pow2_at_least((h->layers[0].taps - 1) * h->layers[0].dil + 1));
+    ring_width.push_back(h->layers[0].cin);
+    for (int b = 1; b <= nb; ++b) {
+        const Layer& kc = h->layers[2 * b - 1];
+        ring_len.push_back(pow2_at_least((kc.taps - 1) * kc.dil + 1));
+        ring_width.push_back(C);
+    }
+    size_t ring_floats = 0;
+    std::vector<size_t> ring_off;
+    for (size_t i = 0; i < ring_len.size(); ++i) {
+        ring_off.push_back(ring_floats);
+        ring_floats += (size_t)ring_len[i] * ring_width[i];
+    }
+    auto cleanup = [&](int rc) {
+        hipFree(st->frames_seen);
+        hipFree(st->in_frame);
+        hipFree(st->out_pose);
+        hipFree(st->rings);
+        hipFree(st->scratch);
+        delete st;
+        return rc;
+    };
+    if (hipMalloc(&st->frames_seen, 16) != hipSuccess || hipMalloc(&st->in_frame, 4 * h->layers[0].cin) != hipSuccess ||
+        hipMalloc(&st->out_pose, 4 * h->layers.back().cout) != hipSuccess ||
+        hipMalloc(&st->rings, 4 * ring_floats) != hipSuccess || hipMalloc(&st->scratch, 8 * (size_t)C) != hipSuccess)
+        return cleanup(fail(VP3D_ERR_OOM, "stream buffers"));
+    hipMemset(st->frames_seen, 0, 16);
+    hipMemset(st->rings, 0, 4 * ring_floats);
+    float* hbuf = st->scratch;           // k-conv output of the current block
+    float* xlast = st->scratch + C;      // output of the last block (or of expand if nb == 0)
+
+    auto W = [&](const Layer& L) -> const void* {
+        return dtype == VP3D_DTYPE_F32 ? (const void*)L.w32 : (dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh);
+    };
+    auto base = [&](const Layer& L) {
+        StreamLayerParams q{};
+        q.W = W(L);
+        q.scale = L.scale;
+        q.shift = L.shift;
+        q.N = L.cout;
+        q.K = L.K;
+        q.Kp = L.Kp;
+        q.cin = L.cin;
+        q.taps = L.taps;
+        q.dil = L.dil;
+        q.relu = L.relu ? 1 : 0;
+        q.frames_seen = st->frames_seen;
+        return q;
+    };
+    // expand: raw-frame ring 0 (+ the new frame) -> ring 1 (block 1 input)
+    {
+        StreamLayerParams q = base(h->layers[0]);
+        q.in = st->rings + ring_off[0];
+        q.in_R = ring_len[0];
+        q.in_frame = st->in_frame;
+        q.in_ring_w = st->rings + ring_off[0];
+        if (nb > 0) {
+            q.out = st->rings + ring_off[1];
+            q.out_R = ring_len[1];
+        } else {
+            q.out = xlast;
+        }
+        st->steps.push_back(q);
+    }
+    for (int b = 1; b <= nb; ++b) {
+        StreamLayerParams k = base(h->layers[2 * b - 1]);
+        k.in = st->rings + ring_off[b];
+        k.in_R = ring_len[b];
+        k.out = hbuf;
+        st->steps.push_back(k);
+        StreamLayerParams pw = base(h->layers[2 * b]);
+        pw.in = hbuf;
+        pw.res = st->rings + ring_off[b];
+        pw.res_R = ring_len[b];
+        if (b < nb) {
+            pw.out = st->rings + ring_off[b + 1];
+            pw.out_R = ring_len[b + 1];
+        } else {
+            pw.out = xlast;
+        }
+        st->steps.push_back(pw);
+    }
+    {
+        StreamLayerParams q = base(h->layers[nl - 1]);
+        q.in = xlast;
+        q.out = st->out_pose;
+        q.advance = 1;
+        st->steps.push_back(q);
+    }
+    *out = st;
+    return VP3D_OK;
+}
+
+int vp3d_stream_reset(vp3d_stream* st, void* stream) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    HIP_TRY(hipMemsetAsync(st->frames_seen, 0, 16, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+int vp3d_stream_io(vp3d_stream* st, float** in_frame, float** out_pose) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (in_frame) *in_frame = st->in_frame;
+    if (out_pose) *out_pose = st->out_pose;
+    return VP3D_OK;
+}
+
+int vp3d_stream_step(vp3d_stream* st, const float* frame, float* pose, void* stream) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    if (frame && frame != st->in_frame)
+        HIP_TRY(hipMemcpyAsync(st->in_frame, frame, 4 * st->h->layers[0].cin, hipMemcpyDeviceToDevice, s));
+    int rc = stream_launch(st, s);
+    if (rc) return rc;
+    if (pose && pose != st->out_pose)
+        HIP_TRY(hipMemcpyAsync(pose, st->out_pose, 4 * st->h->layers.back().cout, hipMemcpyDeviceToDevice, s));
+    return VP3D_OK;
+}
+
+int64_t vp3d_stream_frames_seen(vp3d_stream* st) {
+    if (!st) return -1;
+    int v = -1;
+    if (hipMemcpy(&v, st->frames_seen, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return v;
+}
+
+int vp3d_stream_graph_capture(vp3d_stream* st, void* stream) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (!stream) return fail(VP3D_ERR_ARG, "graph capture needs a non-default stream");
+    hipStream_t s = (hipStream_t)stream;
+    if (st->exec) {
+        hipGraphExecDestroy(st->exec);
+        st->exec = nullptr;
+    }
+    if (st->graph) {
+        hipGraphDestroy(st->graph);
+        st->graph = nullptr;
+    }
+    HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = stream_launch(st, s);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(s, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(VP3D_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    st->graph = g;
+    HIP_TRY(hipGraphInstantiate(&st->exec, g, nullptr, nullptr, 0));
+    return VP3D_OK;
+}
+
+int vp3d_stream_graph_launch(vp3d_stream* st, void* stream) {
+    if (!st || !st->exec) return fail(VP3D_ERR_STATE, "no captured graph");
+    HIP_TRY(hipGraphLaunch(st->exec, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
+int vp3d_stream_destroy(vp3d_stream* st) {
+    if (!st) return VP3D_OK;
+    if (st->exec) hipGraphExecDestroy(st->exec);
+    if (st->graph) hipGraphDestroy(st->graph);
+    hipFree(st->frames_seen);
+    hipFree(st->in_frame);
+    hipFree(st->out_pose);
+    hipFree(st->rings);
+    hipFree(st->scratch);
+    delete st;
+    return VP3D_OK;
+}
+
 // ---- on-device input path ----
 
 int vp3d_normalize_screen(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,

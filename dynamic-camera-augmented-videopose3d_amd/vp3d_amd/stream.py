@@ -1,0 +1,94 @@
+"""Causal streaming inference (BASELINE config 5): one 2D frame in, one 3D pose out.
+
+Wraps vp3d_stream (include/vp3d.h).  For a causal dilated TemporalModel
+(reference TemporalModel.py:79-138 with causal=True), pose k of the stream equals
+frame k of the reference's whole-sequence evaluation of the edge-padded
+sequence (UnchunkedGenerator, generators.py:193-198, causal_shift = pad).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as N
+
+
+class CausalStream:
+    def __init__(self, lifter, dtype: str = "fp16"):
+        """lifter: a NativeLifter (``model.native_lifter()``) of a causal TemporalModel."""
+        self._lib = N.load()
+        self.lifter = lifter
+        self.device = lifter.device
+        self.dtype = dtype
+        self._s = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_stream_create(lifter._h, N.DTYPES[dtype], ctypes.byref(self._s)),
+                    "vp3d_stream_create")
+        fin, fout = ctypes.c_void_p(), ctypes.c_void_p()
+        N.check(self._lib.vp3d_stream_io(self._s, ctypes.byref(fin), ctypes.byref(fout)))
+        self._in_ptr, self._out_ptr = fin.value, fout.value
+        self.n_in = lifter.cfg.num_joints_in * lifter.cfg.in_features
+        self.n_out = lifter.cfg.num_joints_out * 3
+        self._graph_stream = None
+
+    def reset(self) -> None:
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_stream_reset(self._s, N.stream_ptr(self.device)))
+
+    def step(self, frame: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """frame: (J_in, F) float32 on the device -> (J_out, 3) float32."""
+        if not frame.is_cuda:
+            raise RuntimeError("vp3d: stream frames must be HIP device tensors (no CPU fallback)")
+        frame = frame.contiguous().float()
+        assert frame.numel() == self.n_in
+        if out is None:
+            out = torch.empty((self.n_out // 3, 3), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_stream_step(self._s, frame.data_ptr(), out.data_ptr(),
+                                               N.stream_ptr(self.device)), "vp3d_stream_step")
+        return out
+
+    def frames_seen(self) -> int:
+        return int(self._lib.vp3d_stream_frames_seen(self._s))
+
+    # ---- hipGraph replay: the step reads/writes fixed device buffers ----
+    def io_tensors(self):
+        """(in_frame, out_pose) views of the fixed device buffers used by graph replays."""
+        fin = _wrap(self._in_ptr, self.n_in, self.device)
+        fout = _wrap(self._out_ptr, self.n_out, self.device)
+        return fin, fout
+
+    def capture(self, stream: torch.cuda.Stream) -> None:
+        self._graph_stream = stream
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_stream_graph_capture(self._s, stream.cuda_stream),
+                    "vp3d_stream_graph_capture")
+
+    def replay(self, stream: torch.cuda.Stream | None = None) -> None:
+        s = stream if stream is not None else self._graph_stream
+        N.check(self._lib.vp3d_stream_graph_launch(self._s, s.cuda_stream), "vp3d_stream_graph_launch")
+
+    def close(self) -> None:
+        if self._s:
+            self._lib.vp3d_stream_destroy(self._s)
+            self._s = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _DevBuf:
+    """Minimal __cuda_array_interface__ exporter for a raw device pointer."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+def _wrap(ptr: int, n: int, device) -> torch.Tensor:
+    with torch.cuda.device(device):
+        return torch.as_tensor(_DevBuf(ptr, n), device=device)

@@ -121,6 +121,34 @@ int vp3d_layer_count(const vp3d_handle* h);
 int vp3d_profile_read(vp3d_handle* h, double* ms_total, int64_t* launches, double* flop_last);
 int vp3d_profile_reset(vp3d_handle* h);
 
+/* ---- causal streaming (BASELINE config 5) ----
+ * One frame in, one pose out, for a causal dilated model (TemporalModel with
+ * causal=True, TemporalModel.py:107-111): every convolution is a GEMV over taps
+ * read from per-layer ring buffers of past activations.  Output k equals frame k
+ * of the reference's whole-sequence causal evaluation (UnchunkedGenerator edge
+ * padding, generators.py:193-198).  The stream position lives in device memory,
+ * so one step is replayable from a hipGraph. */
+typedef struct vp3d_stream vp3d_stream;
+
+/* dtype: VP3D_DTYPE_* of the weights streamed per step (f16 in config 5). */
+int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out);
+/* Restart the stream (the next frame is frame 0).  Async on `stream`. */
+int vp3d_stream_reset(vp3d_stream* s, void* stream);
+/* Fixed device buffers of the step: the frame to write (J_in*F f32) and the pose
+ * produced (J_out*3 f32).  vp3d_stream_step(s, NULL, NULL, stream) and graph
+ * replays read/write exactly these. */
+int vp3d_stream_io(vp3d_stream* s, float** in_frame, float** out_pose);
+/* One step.  frame / pose: device pointers, or NULL to use the vp3d_stream_io
+ * buffers (frame copied in / pose copied out asynchronously otherwise). */
+int vp3d_stream_step(vp3d_stream* s, const float* frame, float* pose, void* stream);
+/* Frames consumed so far (synchronises with the device). */
+int64_t vp3d_stream_frames_seen(vp3d_stream* s);
+/* Capture one step (io buffers) into a hipGraph on `stream` (must not be the
+ * legacy default stream), then replay it with vp3d_stream_graph_launch. */
+int vp3d_stream_graph_capture(vp3d_stream* s, void* stream);
+int vp3d_stream_graph_launch(vp3d_stream* s, void* stream);
+int vp3d_stream_destroy(vp3d_stream* s);
+
 /* ---- on-device input path (common/camera.py, common/generators.py) ---- */
 
 /* normalize_screen_coordinates (camera.py:14-18): out = X/w*2 - [1, h/w] for

@@ -1,0 +1,73 @@
+"""Causal streaming step (config 5) vs the whole-sequence causal evaluation.
+
+Reference semantics: UnchunkedGenerator pads a causal sequence with 2*pad copies
+of frame 0 in front (generators.py:193-198), and TemporalModel(causal=True) maps
+it to one pose per frame; pose k of the stream must equal frame k of that.
+Tolerances: fp32 stream (f32 FMA GEMVs) within 2e-5 m per coordinate; fp16
+weights within 5 mm, bf16 within 5 cm."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_model
+from oracle.temporal_ref import lifter_forward
+from vp3d_amd import synth
+from vp3d_amd.stream import CausalStream
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(sd, x, fw):
+    pad = (int(np.prod(fw)) - 1) // 2
+    xp = np.concatenate([np.repeat(x[:, :1], 2 * pad, axis=1), x], axis=1)
+    return lifter_forward(sd, xp, list(fw), causal=True).numpy()[0]
+
+
+@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-5), ("fp16", 5e-3), ("bf16", 5e-2)])
+def test_stream_matches_sequence(dtype, tol):
+    fw = (3, 3, 3, 3, 3)
+    m, sd = make_model(False, fw, causal=True)
+    T = 200
+    x = synth.normalized_windows(11, "stream", 1, T)
+    ref = _ref(sd, x, fw)  # (T, 17, 3)
+    m.cuda()
+    st = CausalStream(m.native_lifter(), dtype)
+    xs = torch.from_numpy(x[0]).cuda()
+    out = torch.stack([st.step(xs[t]).clone() for t in range(T)]).cpu().numpy()
+    err = np.abs(out - ref).max()
+    print(f"stream {dtype}: max|d|={err:.3e} m")
+    assert err <= tol
+    assert st.frames_seen() == T
+    st.reset()
+    first = st.step(xs[0]).cpu().numpy()
+    np.testing.assert_allclose(first, out[0], atol=1e-7)
+
+
+def test_stream_graph_replay_matches_eager():
+    fw = (3, 3, 3)
+    m, sd = make_model(False, fw, causal=True, channels=256)
+    T = 60
+    x = torch.from_numpy(synth.normalized_windows(12, "graph", 1, T)[0]).cuda()
+    m.cuda()
+    eager = CausalStream(m.native_lifter(), "fp16")
+    want = torch.stack([eager.step(x[t]).clone() for t in range(T)])
+    g = CausalStream(m.native_lifter(), "fp16")
+    s = torch.cuda.Stream()
+    fin, fout = g.io_tensors()
+    g.capture(s)
+    got = []
+    with torch.cuda.stream(s):
+        for t in range(T):
+            fin.copy_(x[t].reshape(-1))
+            g.replay(s)
+            got.append(fout.clone().view(-1, 3))
+    torch.cuda.synchronize()
+    assert torch.equal(torch.stack(got), want)
+    assert g.frames_seen() == T
+
+
+def test_stream_rejects_noncausal():
+    m, _ = make_model(False, (3, 3), causal=False, channels=64)
+    m.cuda()
+    with pytest.raises(RuntimeError):
+        CausalStream(m.native_lifter(), "fp16")
