@@ -60,14 +60,16 @@ struct StreamLayerParams {
     int N, K, Kp, cin, taps, dil, relu;
     const float* in;          // input ring (in_R slots of cin floats) or plain vector (in_R == 0)
     int in_R;
-    const float* in_frame;    // expand layer: the new frame (read for tap time == t)
+    const float* in_frame;    // expand layer: frame queue (in_frame_R slots), slot t read for tap time t
+    int in_frame_R;
     float* in_ring_w;         // expand layer: ring slot the new frame is appended to
     const float* res;         // residual ring (block input) or nullptr
     int res_R;
     float* out;               // output ring (out_R slots of N floats) or plain vector
     int out_R;
     int* frames_seen;         // device stream position t
-    int advance;              // last layer: single workgroup, t += 1 at the end
+    int advance;              // last layer: the last workgroup to finish does t += 1
+    unsigned* done_counter;   // arrival counter for `advance` (zero between steps)
 };
 hipError_t launch_stream_gemv(const StreamLayerParams& q, Act wtype, hipStream_t s);
 

@@ -19,8 +19,10 @@
 // with fixed kernel arguments.
 //
 // Each kernel is weight-streaming (1 FLOP per weight byte at fp16): the GEMV
-// stages the layer's input vector in LDS and every wave streams whole weight rows
-// with 16-byte loads, several in flight per lane.
+// stages the layer's input vector in LDS and every wave streams one whole weight
+// row with all of its 16-byte loads in flight at once.  Frames come from a device
+// queue indexed by the stream position and poses go to a ring, so one graph can
+// hold several consecutive steps with no host work between them.
 #include "kernels.h"
 
 namespace vp3d {
@@ -52,13 +54,16 @@ __device__ __forceinline__ float wave_sum(float s) {
     return s;
 }
 
-// One streaming GEMV layer.  in: input ring (or plain vector when in_R == 0),
-// optionally the raw input frame for the newest tap of the expand conv.
+// One streaming GEMV layer.  in: input ring (or plain vector when in_R == 0);
+// the expand layer additionally reads the newest frame from the frame queue.
+constexpr int kMaxIter = 8;  // Kp <= 4096 halves: 8 x 512 fp16 elements per row
+
 template <typename WT>
-__global__ __launch_bounds__(1024) void stream_gemv(StreamLayerParams q) {
+__global__ __launch_bounds__(256) void stream_gemv(StreamLayerParams q) {
     __shared__ __attribute__((aligned(16))) float v[kMaxK];
     const int t = *q.frames_seen;
     const int tid = threadIdx.x;
+    const float* frame = q.in_frame ? q.in_frame + (int64_t)(t & (q.in_frame_R - 1)) * q.cin : nullptr;
 
     // stage the input vector: tap k reads stream time t - (taps-1-k)*dil, clamped at 0
     for (int kk = tid; kk < q.Kp; kk += blockDim.x) {
@@ -68,8 +73,8 @@ __global__ __launch_bounds__(1024) void stream_gemv(StreamLayerParams q) {
             const int c = kk - tap * q.cin;
             int tt = t - (q.taps - 1 - tap) * q.dil;
             tt = tt < 0 ? 0 : tt;
-            if (q.in_frame && tt == t)
-                val = q.in_frame[c];
+            if (frame && tt == t)
+                val = frame[c];
             else if (q.in_R)
                 val = q.in[(int64_t)(tt & (q.in_R - 1)) * q.cin + c];
             else
@@ -78,34 +83,42 @@ __global__ __launch_bounds__(1024) void stream_gemv(StreamLayerParams q) {
         v[kk] = val;
     }
     // the expand layer also appends the new frame to its input ring (slot of time t;
-    // the other taps of this step read older slots, so no workgroup races with it)
-    if (q.in_frame && q.in_ring_w && blockIdx.x == 0)
+    // this step's other taps read older slots, so no workgroup races with it)
+    if (frame && q.in_ring_w && blockIdx.x == 0)
         for (int c = tid; c < q.cin; c += blockDim.x)
-            q.in_ring_w[(int64_t)(t & (q.in_R - 1)) * q.cin + c] = q.in_frame[c];
+            q.in_ring_w[(int64_t)(t & (q.in_R - 1)) * q.cin + c] = frame[c];
     __syncthreads();
 
     const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int nwaves = blockDim.x >> 6;
-    for (int n = blockIdx.x * nwaves + wave; n < q.N; n += gridDim.x * nwaves) {
+    const int n = blockIdx.x * (blockDim.x >> 6) + (tid >> 6);
+    if (n < q.N) {
         float s = 0.f;
         if constexpr (sizeof(WT) == 2) {
-            const WT* wr = (const WT*)q.W + (int64_t)n * q.Kp;
-            // 512 elements per wave-iteration: each lane 8 (16 bytes)
-            for (int k0 = 0; k0 < q.Kp; k0 += 512) {
-                const int k = k0 + lane * 8;
-                if (k < q.Kp) s += wdot8<WT>(*(const u32x4*)(wr + k), &v[k]);
-            }
+            // whole row in flight at once: up to 8 x 16-byte loads per lane
+            const WT* wr = (const WT*)q.W + (int64_t)n * q.Kp + lane * 8;
+            u32x4 w[kMaxIter];
+#pragma unroll
+            for (int it = 0; it < kMaxIter; ++it)
+                if (it * 512 + lane * 8 < q.Kp) w[it] = *(const u32x4*)(wr + it * 512);
+#pragma unroll
+            for (int it = 0; it < kMaxIter; ++it)
+                if (it * 512 + lane * 8 < q.Kp) s += wdot8<WT>(w[it], &v[it * 512 + lane * 8]);
         } else {
-            const float* wr = (const float*)q.W + (int64_t)n * q.Kp;
-            for (int k0 = 0; k0 < q.Kp; k0 += 256) {
-                const int k = k0 + lane * 4;
-                if (k < q.Kp) {
-                    const float4 w4 = *(const float4*)(wr + k);
-                    s = __builtin_fmaf(w4.x, v[k], s);
-                    s = __builtin_fmaf(w4.y, v[k + 1], s);
-                    s = __builtin_fmaf(w4.z, v[k + 2], s);
-                    s = __builtin_fmaf(w4.w, v[k + 3], s);
+            const float* wr = (const float*)q.W + (int64_t)n * q.Kp + lane * 4;
+            for (int k0 = 0; k0 < q.Kp; k0 += 256 * 4) {
+                float4 w4[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (k0 + u * 256 + lane * 4 < q.Kp) w4[u] = *(const float4*)(wr + k0 + u * 256);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + u * 256 + lane * 4;
+                    if (k < q.Kp) {
+                        s = __builtin_fmaf(w4[u].x, v[k], s);
+                        s = __builtin_fmaf(w4[u].y, v[k + 1], s);
+                        s = __builtin_fmaf(w4[u].z, v[k + 2], s);
+                        s = __builtin_fmaf(w4[u].w, v[k + 3], s);
+                    }
                 }
             }
         }
@@ -119,10 +132,17 @@ __global__ __launch_bounds__(1024) void stream_gemv(StreamLayerParams q) {
         }
     }
     if (q.advance) {
-        // last layer of the step: one workgroup; advance the stream position after
-        // every wave has read it
+        // last layer of the step: the last workgroup to finish advances the stream
+        // position (every workgroup read t before its arrival is counted)
         __syncthreads();
-        if (tid == 0) *q.frames_seen = t + 1;
+        if (tid == 0) {
+            const unsigned done = __hip_atomic_fetch_add(q.done_counter, 1u, __ATOMIC_ACQ_REL,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+            if (done == gridDim.x - 1) {
+                *q.done_counter = 0u;
+                __hip_atomic_store(q.frames_seen, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 }
 
@@ -130,13 +150,9 @@ __global__ __launch_bounds__(1024) void stream_gemv(StreamLayerParams q) {
 
 hipError_t launch_stream_gemv(const StreamLayerParams& q, Act wtype, hipStream_t s) {
     if (q.Kp > kMaxK) return hipErrorInvalidValue;
-    const int nwaves = 4;
-    int grid = (q.N + nwaves - 1) / nwaves;
-    dim3 block(256);
-    if (q.advance) {  // single workgroup of 16 waves
-        grid = 1;
-        block = dim3(1024);
-    }
+    const int nwaves = 4;  // one output row per wave
+    const int grid = (q.N + nwaves - 1) / nwaves;
+    const dim3 block(64 * nwaves);
     if (wtype == Act::F32)
         hipLaunchKernelGGL(stream_gemv<float>, dim3(grid), block, 0, s, q);
     else if (wtype == Act::F16)

@@ -594,9 +594,11 @@ int vp3d_profile_read(vp3d_handle* h, double* ms_total, int64_t* launches, doubl
 struct vp3d_stream {
     vp3d_handle* h = nullptr;
     int dtype = VP3D_DTYPE_F16;
-    int* frames_seen = nullptr;        // device
-    float* in_frame = nullptr;         // device, J_in*F
-    float* out_pose = nullptr;         // device, J_out*3
+    int* frames_seen = nullptr;        // device stream position + arrival counter
+    float* in_frame = nullptr;         // device frame queue, kQueue x J_in*F
+    float* out_pose = nullptr;         // device pose ring, kQueue x J_out*3
+    int64_t host_t = 0;                // host mirror of the stream position
+    int graph_steps = 0;
     float* rings = nullptr;            // all ring buffers
     float* scratch = nullptr;          // k-conv output, last block output
     std::vector<StreamLayerParams> steps;
@@ -605,6 +607,8 @@ struct vp3d_stream {
 };
 
 namespace {
+
+constexpr int kQueue = 64;
 
 int pow2_at_least(int v) {
     int r = 1;
@@ -664,8 +668,9 @@ int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
         delete st;
         return rc;
     };
-    if (hipMalloc(&st->frames_seen, 16) != hipSuccess || hipMalloc(&st->in_frame, 4 * h->layers[0].cin) != hipSuccess ||
-        hipMalloc(&st->out_pose, 4 * h->layers.back().cout) != hipSuccess ||
+    if (hipMalloc(&st->frames_seen, 16) != hipSuccess ||
+        hipMalloc(&st->in_frame, 4 * (size_t)kQueue * h->layers[0].cin) != hipSuccess ||
+        hipMalloc(&st->out_pose, 4 * (size_t)kQueue * h->layers.back().cout) != hipSuccess ||
         hipMalloc(&st->rings, 4 * ring_floats) != hipSuccess || hipMalloc(&st->scratch, 8 * (size_t)C) != hipSuccess)
         return cleanup(fail(VP3D_ERR_OOM, "stream buffers"));
     hipMemset(st->frames_seen, 0, 16);
@@ -697,6 +702,7 @@ int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
         q.in = st->rings + ring_off[0];
         q.in_R = ring_len[0];
         q.in_frame = st->in_frame;
+        q.in_frame_R = kQueue;
         q.in_ring_w = st->rings + ring_off[0];
         if (nb > 0) {
             q.out = st->rings + ring_off[1];
@@ -728,7 +734,9 @@ int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
         StreamLayerParams q = base(h->layers[nl - 1]);
         q.in = xlast;
         q.out = st->out_pose;
+        q.out_R = kQueue;
         q.advance = 1;
+        q.done_counter = (unsigned*)(st->frames_seen + 1);
         st->steps.push_back(q);
     }
     *out = st;
@@ -738,25 +746,32 @@ int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
 int vp3d_stream_reset(vp3d_stream* st, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     HIP_TRY(hipMemsetAsync(st->frames_seen, 0, 16, (hipStream_t)stream));
+    st->host_t = 0;
     return VP3D_OK;
 }
 
-int vp3d_stream_io(vp3d_stream* st, float** in_frame, float** out_pose) {
+int vp3d_stream_io(vp3d_stream* st, float** in_frames, float** out_poses, int* queue_len) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
-    if (in_frame) *in_frame = st->in_frame;
-    if (out_pose) *out_pose = st->out_pose;
+    if (in_frames) *in_frames = st->in_frame;
+    if (out_poses) *out_poses = st->out_pose;
+    if (queue_len) *queue_len = kQueue;
     return VP3D_OK;
 }
 
 int vp3d_stream_step(vp3d_stream* st, const float* frame, float* pose, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     hipStream_t s = (hipStream_t)stream;
-    if (frame && frame != st->in_frame)
-        HIP_TRY(hipMemcpyAsync(st->in_frame, frame, 4 * st->h->layers[0].cin, hipMemcpyDeviceToDevice, s));
+    const int slot = (int)(st->host_t % kQueue);
+    const int cin = st->h->layers[0].cin, cout = st->h->layers.back().cout;
+    if (frame)
+        HIP_TRY(hipMemcpyAsync(st->in_frame + (size_t)slot * cin, frame, 4 * cin,
+                               hipMemcpyDeviceToDevice, s));
     int rc = stream_launch(st, s);
     if (rc) return rc;
-    if (pose && pose != st->out_pose)
-        HIP_TRY(hipMemcpyAsync(pose, st->out_pose, 4 * st->h->layers.back().cout, hipMemcpyDeviceToDevice, s));
+    if (pose)
+        HIP_TRY(hipMemcpyAsync(pose, st->out_pose + (size_t)slot * cout, 4 * cout,
+                               hipMemcpyDeviceToDevice, s));
+    st->host_t += 1;
     return VP3D_OK;
 }
 
@@ -767,9 +782,10 @@ int64_t vp3d_stream_frames_seen(vp3d_stream* st) {
     return v;
 }
 
-int vp3d_stream_graph_capture(vp3d_stream* st, void* stream) {
+int vp3d_stream_graph_capture(vp3d_stream* st, void* stream, int steps) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     if (!stream) return fail(VP3D_ERR_ARG, "graph capture needs a non-default stream");
+    if (steps < 1) return fail(VP3D_ERR_ARG, "steps must be >= 1");
     hipStream_t s = (hipStream_t)stream;
     if (st->exec) {
         hipGraphExecDestroy(st->exec);
@@ -780,12 +796,14 @@ int vp3d_stream_graph_capture(vp3d_stream* st, void* stream) {
         st->graph = nullptr;
     }
     HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    int rc = stream_launch(st, s);
+    int rc = VP3D_OK;
+    for (int i = 0; i < steps && rc == VP3D_OK; ++i) rc = stream_launch(st, s);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(s, &g);
     if (rc) return rc;
     if (e != hipSuccess) return fail(VP3D_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
     st->graph = g;
+    st->graph_steps = steps;
     HIP_TRY(hipGraphInstantiate(&st->exec, g, nullptr, nullptr, 0));
     return VP3D_OK;
 }
@@ -793,6 +811,7 @@ int vp3d_stream_graph_capture(vp3d_stream* st, void* stream) {
 int vp3d_stream_graph_launch(vp3d_stream* st, void* stream) {
     if (!st || !st->exec) return fail(VP3D_ERR_STATE, "no captured graph");
     HIP_TRY(hipGraphLaunch(st->exec, (hipStream_t)stream));
+    st->host_t += st->graph_steps;
     return VP3D_OK;
 }
 

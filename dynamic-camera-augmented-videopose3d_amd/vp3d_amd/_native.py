@@ -96,10 +96,10 @@ _SIGNATURES = {
     "vp3d_mpjpe_accumulate": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "vp3d_stream_create": (_int, [_vp, _int, ctypes.POINTER(_vp)]),
     "vp3d_stream_reset": (_int, [_vp, _vp]),
-    "vp3d_stream_io": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
+    "vp3d_stream_io": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_int)]),
     "vp3d_stream_step": (_int, [_vp, _vp, _vp, _vp]),
     "vp3d_stream_frames_seen": (ctypes.c_int64, [_vp]),
-    "vp3d_stream_graph_capture": (_int, [_vp, _vp]),
+    "vp3d_stream_graph_capture": (_int, [_vp, _vp, _int]),
     "vp3d_stream_graph_launch": (_int, [_vp, _vp]),
     "vp3d_stream_destroy": (_int, [_vp]),
     "vp3d_last_error": (ctypes.c_char_p, []),

@@ -25,9 +25,9 @@ class CausalStream:
         with torch.cuda.device(self.device):
             N.check(self._lib.vp3d_stream_create(lifter._h, N.DTYPES[dtype], ctypes.byref(self._s)),
                     "vp3d_stream_create")
-        fin, fout = ctypes.c_void_p(), ctypes.c_void_p()
-        N.check(self._lib.vp3d_stream_io(self._s, ctypes.byref(fin), ctypes.byref(fout)))
-        self._in_ptr, self._out_ptr = fin.value, fout.value
+        fin, fout, q = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int()
+        N.check(self._lib.vp3d_stream_io(self._s, ctypes.byref(fin), ctypes.byref(fout), ctypes.byref(q)))
+        self._in_ptr, self._out_ptr, self.queue_len = fin.value, fout.value, q.value
         self.n_in = lifter.cfg.num_joints_in * lifter.cfg.in_features
         self.n_out = lifter.cfg.num_joints_out * 3
         self._graph_stream = None
@@ -52,17 +52,20 @@ class CausalStream:
     def frames_seen(self) -> int:
         return int(self._lib.vp3d_stream_frames_seen(self._s))
 
-    # ---- hipGraph replay: the step reads/writes fixed device buffers ----
+    # ---- hipGraph replay: steps read the device frame queue, write the pose ring ----
     def io_tensors(self):
-        """(in_frame, out_pose) views of the fixed device buffers used by graph replays."""
-        fin = _wrap(self._in_ptr, self.n_in, self.device)
-        fout = _wrap(self._out_ptr, self.n_out, self.device)
+        """(frame_queue (Q, J_in*F), pose_ring (Q, J_out*3)) views of the device buffers:
+        step t reads frame slot t % Q and writes pose slot t % Q."""
+        Q = self.queue_len
+        fin = _wrap(self._in_ptr, Q * self.n_in, self.device).view(Q, self.n_in)
+        fout = _wrap(self._out_ptr, Q * self.n_out, self.device).view(Q, self.n_out)
         return fin, fout
 
-    def capture(self, stream: torch.cuda.Stream) -> None:
+    def capture(self, stream: torch.cuda.Stream, steps: int = 1) -> None:
+        """Capture `steps` consecutive steps into one hipGraph."""
         self._graph_stream = stream
         with torch.cuda.device(self.device):
-            N.check(self._lib.vp3d_stream_graph_capture(self._s, stream.cuda_stream),
+            N.check(self._lib.vp3d_stream_graph_capture(self._s, stream.cuda_stream, int(steps)),
                     "vp3d_stream_graph_capture")
 
     def replay(self, stream: torch.cuda.Stream | None = None) -> None:

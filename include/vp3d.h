@@ -134,18 +134,19 @@ typedef struct vp3d_stream vp3d_stream;
 int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out);
 /* Restart the stream (the next frame is frame 0).  Async on `stream`. */
 int vp3d_stream_reset(vp3d_stream* s, void* stream);
-/* Fixed device buffers of the step: the frame to write (J_in*F f32) and the pose
- * produced (J_out*3 f32).  vp3d_stream_step(s, NULL, NULL, stream) and graph
- * replays read/write exactly these. */
-int vp3d_stream_io(vp3d_stream* s, float** in_frame, float** out_pose);
-/* One step.  frame / pose: device pointers, or NULL to use the vp3d_stream_io
- * buffers (frame copied in / pose copied out asynchronously otherwise). */
+/* Device frame queue and pose ring of the stream (queue_len slots each, a power of
+ * two): step t reads frame slot t % queue_len and writes pose slot t % queue_len.
+ * Graph replays read/write exactly these; frames can be queued ahead of time. */
+int vp3d_stream_io(vp3d_stream* s, float** in_frames, float** out_poses, int* queue_len);
+/* One step.  frame / pose: device pointers (frame copied into the queue slot of
+ * this step, pose copied out of it, asynchronously), or NULL to use the queue
+ * slot as is. */
 int vp3d_stream_step(vp3d_stream* s, const float* frame, float* pose, void* stream);
 /* Frames consumed so far (synchronises with the device). */
 int64_t vp3d_stream_frames_seen(vp3d_stream* s);
-/* Capture one step (io buffers) into a hipGraph on `stream` (must not be the
- * legacy default stream), then replay it with vp3d_stream_graph_launch. */
-int vp3d_stream_graph_capture(vp3d_stream* s, void* stream);
+/* Capture `steps` consecutive steps (frames from the queue) into a hipGraph on
+ * `stream` (not the legacy default stream); replay with vp3d_stream_graph_launch. */
+int vp3d_stream_graph_capture(vp3d_stream* s, void* stream, int steps);
 int vp3d_stream_graph_launch(vp3d_stream* s, void* stream);
 int vp3d_stream_destroy(vp3d_stream* s);
 

@@ -44,26 +44,33 @@ def test_stream_matches_sequence(dtype, tol):
 
 
 def test_stream_graph_replay_matches_eager():
+    """Graphs of 1 and of 8 steps fed from the device frame queue reproduce the
+    eager per-step results bit for bit."""
     fw = (3, 3, 3)
     m, sd = make_model(False, fw, causal=True, channels=256)
-    T = 60
-    x = torch.from_numpy(synth.normalized_windows(12, "graph", 1, T)[0]).cuda()
+    T = 80
+    x = torch.from_numpy(synth.normalized_windows(12, "graph", 1, T)[0]).cuda().reshape(T, -1)
     m.cuda()
     eager = CausalStream(m.native_lifter(), "fp16")
-    want = torch.stack([eager.step(x[t]).clone() for t in range(T)])
-    g = CausalStream(m.native_lifter(), "fp16")
-    s = torch.cuda.Stream()
-    fin, fout = g.io_tensors()
-    g.capture(s)
-    got = []
-    with torch.cuda.stream(s):
-        for t in range(T):
-            fin.copy_(x[t].reshape(-1))
-            g.replay(s)
-            got.append(fout.clone().view(-1, 3))
-    torch.cuda.synchronize()
-    assert torch.equal(torch.stack(got), want)
-    assert g.frames_seen() == T
+    want = torch.stack([eager.step(x[t]).clone().reshape(-1) for t in range(T)])
+    for G in (1, 8):
+        g = CausalStream(m.native_lifter(), "fp16")
+        Q = g.queue_len
+        assert T % G == 0 and Q % G == 0
+        s = torch.cuda.Stream()
+        fq, pr = g.io_tensors()
+        g.capture(s, steps=G)
+        got = []
+        with torch.cuda.stream(s):
+            for t0 in range(0, T, G):
+                for t in range(t0, t0 + G):
+                    fq[t % Q].copy_(x[t])
+                g.replay(s)
+                for t in range(t0, t0 + G):
+                    got.append(pr[t % Q].clone())
+        torch.cuda.synchronize()
+        assert torch.equal(torch.stack(got), want), G
+        assert g.frames_seen() == T
 
 
 def test_stream_rejects_noncausal():

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Aggregate rocprofv3 --pmc counter CSVs per (kernel, grid) = per lifter layer.
+
+    python tools/pmc_summary.py gpurun_out/TAG [--batch 8192]
+
+Reads every pmc*/**/run_counter_collection.csv under the directory, averages each
+counter over the dispatches of one (kernel, grid size), and prints a table.
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB;
+on gfx950 FETCH_SIZE counts 128-B requests as 64 B, so the read side is doubled
+(`fetch_bytes_corrected`).  Effective clock = GRBM_GUI_ACTIVE / 8 XCDs / duration.
+"""
+import argparse
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from prof_summary import layer_table, short  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--batch", type=int, default=8192)
+    a = ap.parse_args()
+    vals = defaultdict(lambda: defaultdict(list))
+    durs = defaultdict(list)
+    for f in glob.glob(os.path.join(a.dir, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                key = (short(r["Kernel_Name"]), int(r["Grid_Size"]) if "Grid_Size" in r else int(r.get("Grid_Size_X", 0)))
+                vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    lt = layer_table(a.batch)
+    counters = sorted({c for v in vals.values() for c in v})
+    print("| kernel | grid | layer | " + " | ".join(counters) + " |")
+    print("|---|---|---|" + "---|" * len(counters))
+    for (k, g), cs in sorted(vals.items(), key=lambda kv: -kv[0][1]):
+        if not k.startswith("conv_gemm") and "stream" not in k and "pack" not in k:
+            continue
+        row = []
+        for c in counters:
+            v = cs.get(c)
+            row.append(f"{sum(v) / len(v):.4g}" if v else "")
+        print(f"| {k} | {g} | {'/'.join(lt.get(g, ['-']))} | " + " | ".join(row) + " |")
+
+
+if __name__ == "__main__":
+    main()
