@@ -61,27 +61,33 @@ constexpr int kMaxIter = 8;  // Kp <= 4096 halves: 8 x 512 fp16 elements per row
 template <typename WT>
 __global__ __launch_bounds__(256) void stream_gemv(StreamLayerParams q) {
     __shared__ __attribute__((aligned(16))) float v[kMaxK];
-    const int t = *q.frames_seen;
     const int tid = threadIdx.x;
-    const float* frame = q.in_frame ? q.in_frame + (int64_t)(t & (q.in_frame_R - 1)) * q.cin : nullptr;
+    const int lane = tid & 63;
+    const int n = blockIdx.x * (blockDim.x >> 6) + (tid >> 6);
 
-    // stage the input vector: tap k reads stream time t - (taps-1-k)*dil, clamped at 0
-    for (int kk = tid; kk < q.Kp; kk += blockDim.x) {
-        float val = 0.f;
-        if (kk < q.K) {
-            const int tap = kk / q.cin;
-            const int c = kk - tap * q.cin;
-            int tt = t - (q.taps - 1 - tap) * q.dil;
-            tt = tt < 0 ? 0 : tt;
-            if (frame && tt == t)
-                val = frame[c];
-            else if (q.in_R)
-                val = q.in[(int64_t)(tt & (q.in_R - 1)) * q.cin + c];
-            else
-                val = q.in[c];
+    // 1. the weight row does not depend on the stream position: put all of its
+    //    16-byte loads in flight first, so their latency overlaps the staging below
+    u32x4 w[kMaxIter];
+    if constexpr (sizeof(WT) == 2) {
+        if (n < q.N) {
+            const WT* wr = (const WT*)q.W + (int64_t)n * q.Kp + lane * 8;
+#pragma unroll
+            for (int it = 0; it < kMaxIter; ++it)
+                if (it * 512 + lane * 8 < q.Kp) w[it] = *(const u32x4*)(wr + it * 512);
         }
-        v[kk] = val;
     }
+
+    // 2. stage the input vector: tap k reads stream time t - (taps-1-k)*dil, clamped at 0
+    const int t = *q.frames_seen;
+    const float* frame = q.in_frame ? q.in_frame + (int64_t)(t & (q.in_frame_R - 1)) * q.cin : nullptr;
+    for (int tap = 0; tap < q.taps; ++tap) {
+        int tt = t - (q.taps - 1 - tap) * q.dil;
+        tt = tt < 0 ? 0 : tt;
+        const float* src = (frame && tt == t) ? frame
+                           : (q.in_R ? q.in + (int64_t)(tt & (q.in_R - 1)) * q.cin : q.in);
+        for (int c = tid; c < q.cin; c += blockDim.x) v[tap * q.cin + c] = src[c];
+    }
+    for (int kk = q.K + tid; kk < q.Kp; kk += blockDim.x) v[kk] = 0.f;
     // the expand layer also appends the new frame to its input ring (slot of time t;
     // this step's other taps read older slots, so no workgroup races with it)
     if (frame && q.in_ring_w && blockIdx.x == 0)
@@ -89,17 +95,10 @@ __global__ __launch_bounds__(256) void stream_gemv(StreamLayerParams q) {
             q.in_ring_w[(int64_t)(t & (q.in_R - 1)) * q.cin + c] = frame[c];
     __syncthreads();
 
-    const int lane = tid & 63;
-    const int n = blockIdx.x * (blockDim.x >> 6) + (tid >> 6);
+    // 3. dot products
     if (n < q.N) {
         float s = 0.f;
         if constexpr (sizeof(WT) == 2) {
-            // whole row in flight at once: up to 8 x 16-byte loads per lane
-            const WT* wr = (const WT*)q.W + (int64_t)n * q.Kp + lane * 8;
-            u32x4 w[kMaxIter];
-#pragma unroll
-            for (int it = 0; it < kMaxIter; ++it)
-                if (it * 512 + lane * 8 < q.Kp) w[it] = *(const u32x4*)(wr + it * 512);
 #pragma unroll
             for (int it = 0; it < kMaxIter; ++it)
                 if (it * 512 + lane * 8 < q.Kp) s += wdot8<WT>(w[it], &v[it * 512 + lane * 8]);

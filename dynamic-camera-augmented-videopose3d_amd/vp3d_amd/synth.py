@@ -160,3 +160,29 @@ def gt_poses(seed: int, name: str, n_frames: int, n_joints: int = 17) -> np.ndar
 CMU_INTRINSICS = {"focal_length": np.array([1.5625, 1.5625], dtype=np.float32),
                   "center": np.array([0.0, 0.0], dtype=np.float32),
                   "res_w": 1280, "res_h": 720}
+
+
+def synthetic_split(n_subjects: int, n_actions: int, frames: int, joints: int, seed: int,
+                    normalize) -> dict:
+    """A CMU-style evaluation split {subject: {action: {'positions_3d', 'keypoints',
+    'cameras'}}}: random-walk 2D tracks normalised with `normalize(X, w, h)` (the
+    reference's normalize_screen_coordinates semantics, 1280x720), root-relative 3D
+    (run.py:73, quirk Q3), per-frame procedural extrinsics and motion statistics.
+    Sequence lengths differ per action/subject (ragged)."""
+    data = {}
+    for si in range(n_subjects):
+        subj = f"S{si + 1}"
+        data[subj] = {}
+        for ai in range(n_actions):
+            name = f"Action{ai} {si}"
+            T = frames + 37 * ai + 11 * si
+            key = f"{seed}/{subj}/{ai}"
+            kps = np.asarray(normalize(keypoint_tracks(seed + 1, key, T, joints), 1280, 720),
+                             dtype=np.float32)
+            mot = uniform(seed + 4, key, (4, 3), -1.0, 1.0)
+            cams = {"intrinsics": CMU_INTRINSICS, "extrinsics": camera_extrinsics(seed + 2, key, T),
+                    "cam_velocity": mot[0], "cam_acceleration": mot[1],
+                    "cam_angular_velocity": mot[2], "cam_angular_acceleration": mot[3]}
+            data[subj][name] = {"positions_3d": gt_poses(seed + 3, key, T, joints),
+                                "keypoints": kps, "cameras": cams}
+    return data

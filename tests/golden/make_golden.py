@@ -177,7 +177,57 @@ def loss_goldens():
     save("loss", **a)
 
 
+def run_eval_golden():
+    """The reference's FCN --evaluate loop (run.py:697-771, 906-971) on the seeded
+    synthetic split, 27-frame RF, 1024 channels (BASELINE config 1 shape)."""
+    data = synth.synthetic_split(3, 3, 200, 17, 0, ref_camera.normalize_screen_coordinates)
+    fw = [3, 3, 3]
+    m, sd, keys = build_ref_model(False, fw, channels=1024, seed=0)
+    pad = (m.receptive_field() - 1) // 2
+    actions = {}
+    for s in data:
+        for a in data[s]:
+            actions.setdefault(a.split(" ")[0], []).append((s, a))
+    out = {}
+    e1_seq, infos, motion = [], [], []
+    for key, seqs in actions.items():
+        cams = [data[s][a]["cameras"] for s, a in seqs]
+        p3d = [data[s][a]["positions_3d"] for s, a in seqs]
+        p2d = [data[s][a]["keypoints"] for s, a in seqs]
+        gen = ref_gen.UnchunkedGenerator(cams, p3d, p2d, pad=pad, causal_shift=0)
+        e1 = e2 = e3 = ev = 0.0
+        N = 0
+        with torch.no_grad():
+            for bc, b3, b2, info in gen.next_epoch():
+                x2 = torch.from_numpy(b2.astype("float32"))
+                x3 = torch.from_numpy(b3.astype("float32"))
+                pred = m(x2)
+                err = ref_loss.mpjpe(pred, x3)
+                n = x3.shape[0] * x3.shape[1]
+                e3 += n * ref_loss.n_mpjpe(pred, x3).item()
+                e1 += n * err.item()
+                e1_seq.append(err.numpy())
+                infos.append(info)
+                pm = np.linalg.norm(np.diff(b3, axis=1), axis=-1)
+                motion.append(np.mean(pm.squeeze(), axis=(0, 1)))
+                N += n
+                inp = x3.numpy().reshape(-1, 17, 3)
+                pr = pred.numpy().reshape(-1, 17, 3)
+                e2 += n * ref_loss.p_mpjpe(pr, inp)
+                ev += n * ref_loss.mean_velocity_error(pr, inp)
+        # run.py:762-765 evaluates (loss / N) * 1000 on the accumulators' own scalar types
+        out[key] = np.array([(e1 / N) * 1000, (e2 / N) * 1000, (e3 / N) * 1000, (ev / N) * 1000])
+    corr = np.corrcoef(np.stack([np.array(e1_seq)] + [
+        np.linalg.norm(np.array([i[k] for i in infos]), axis=1)
+        for k in ("cam_velocity", "cam_acceleration", "cam_angular_velocity", "cam_angular_acceleration")]
+        + [np.array(motion)], axis=1))
+    save("run_eval_27", actions=np.array(list(out.keys())), errors=np.stack(list(out.values())),
+         pmcc=corr[0, 1:6], meta=np.array(json.dumps(dict(fw=fw, channels=1024, seed=0,
+                                                           subjects=3, actions=3, frames=200))))
+
+
 if __name__ == "__main__":
+    run_eval_golden()
     model_goldens()
     generator_goldens()
     camera_goldens()
