@@ -337,7 +337,11 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     if (a_type != Act::F32 && a_type != compute) return hipErrorInvalidValue;
     if (out_type != Act::F32 && out_type != compute) return hipErrorInvalidValue;
     if (conv_gemm_big_eligible(p, a_type, out_type, compute))
-        return launch_conv_gemm_big(p, out_type, compute, stream);
+        switch (big_schedule()) {
+            case 1: return launch_conv_gemm_persist(p, out_type, compute, stream);
+            case 2: return launch_conv_gemm_pp(p, out_type, compute, stream);
+            default: return launch_conv_gemm_big(p, out_type, compute, stream);
+        }
     const int aes = a_type == Act::F32 ? 4 : 2;
     int amode = A_SCALAR;
     if ((p.Ktap % kH16Bk == 0) && (p.lda % 8 == 0) && aligned(p.A, 16))

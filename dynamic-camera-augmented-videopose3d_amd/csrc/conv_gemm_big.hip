@@ -336,6 +336,17 @@ int big_tile_n() {
 
 }  // namespace
 
+int big_schedule() {
+    static int v = [] {
+        const char* e = getenv("VP3D_GEMM");
+        if (big_tile_n() != 256 || !e) return 0;
+        if (!strcmp(e, "persist")) return 1;
+        if (!strcmp(e, "pp")) return 2;
+        return 0;
+    }();
+    return v;
+}
+
 bool conv_gemm_big_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
     if (compute == Act::F32 || a_type != compute) return false;
     if (out_type != Act::F32 && out_type != compute) return false;

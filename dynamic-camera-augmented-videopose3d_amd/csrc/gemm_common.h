@@ -148,11 +148,21 @@ __device__ __forceinline__ void epilogue_scalar(const ConvGemmParams& p, const f
 // tile through its own LDS region (row pitch 68 floats: conflict-free writes),
 // then every lane owns 8 consecutive columns of a row: 16/32-byte residual loads
 // and output stores, whole 128-byte lines per 8 lanes.
+//
+// No workgroup barrier inside: the staging region is private to the wave and one
+// wave's LDS instructions retire in issue order, so a compiler fence orders the
+// transpose.  (A __syncthreads here would also wait for every global store issued
+// so far, serialising the passes on store completion.)  The residual rows of pass
+// k+1 are loaded before the stores of pass k, so waiting for them never waits for
+// those stores either.
 constexpr int kEpiLd = 68;
 
 template <typename OT, int MI, int PASS_ROWS>
 __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x4 (&acc)[MI][4],
                                              float* stage, int mw, int nw, int lane) {
+    constexpr int NP = MI * 16 / PASS_ROWS;  // passes
+    constexpr int NQ = PASS_ROWS / 8;        // rows per lane per pass
+    constexpr int RW = sizeof(OT) == 2 ? 1 : 2;  // 16-byte words per 8 outputs
     const int c8 = lane & 7;
     const int n = nw + c8 * 8;
     const bool nval = n < p.N;
@@ -162,8 +172,24 @@ __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x
         sc[e] = nval ? p.scale[n + e] : 0.f;
         sh[e] = nval ? p.shift[n + e] : 0.f;
     }
+    u32x4 res[2][NQ][RW];
+    auto load_res = [&](int pass, u32x4 (&r)[NQ][RW]) {
 #pragma unroll
-    for (int pass = 0; pass < MI * 16 / PASS_ROWS; ++pass) {
+        for (int q = 0; q < NQ; ++q) {
+            const int m = mw + pass * PASS_ROWS + q * 8 + (lane >> 3);
+            if (p.R && m < p.M && nval) {
+                const OT* rp = (const OT*)p.R + (int64_t)res_row(p, m) * p.ldr + n;
+#pragma unroll
+                for (int w = 0; w < RW; ++w) r[q][w] = *(const u32x4*)(rp + w * (16 / sizeof(OT)));
+            } else {
+#pragma unroll
+                for (int w = 0; w < RW; ++w) r[q][w] = u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+    };
+    load_res(0, res[0]);
+#pragma unroll
+    for (int pass = 0; pass < NP; ++pass) {
 #pragma unroll
         for (int ii = 0; ii < PASS_ROWS / 16; ++ii) {
             const int i = pass * (PASS_ROWS / 16) + ii;
@@ -173,9 +199,10 @@ __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x
                 for (int r = 0; r < 4; ++r)
                     stage[(ii * 16 + (lane >> 4) * 4 + r) * kEpiLd + j * 16 + (lane & 15)] = acc[i][j][r];
         }
-        __syncthreads();
+        asm volatile("" ::: "memory");
+        if (pass + 1 < NP) load_res(pass + 1, res[(pass + 1) & 1]);
 #pragma unroll
-        for (int q = 0; q < PASS_ROWS / 8; ++q) {
+        for (int q = 0; q < NQ; ++q) {
             const int row = q * 8 + (lane >> 3);
             const int m = mw + pass * PASS_ROWS + row;
             const f32x4 lo = *(const f32x4*)&stage[row * kEpiLd + c8 * 8];
@@ -188,16 +215,15 @@ __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x
                     if (p.relu) v[e] = v[e] > 0.f ? v[e] : 0.f;
                 }
                 if (p.R) {
-                    const int64_t ro = (int64_t)res_row(p, m) * p.ldr + n;
+                    const u32x4(&rq)[RW] = res[pass & 1][q];
                     if constexpr (sizeof(OT) == 2) {
-                        const u32x4 rv = *(const u32x4*)((const OT*)p.R + ro);
                         typedef OT ot8 __attribute__((ext_vector_type(8)));
-                        const ot8 r8 = __builtin_bit_cast(ot8, rv);
+                        const ot8 r8 = __builtin_bit_cast(ot8, rq[0]);
 #pragma unroll
                         for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
                     } else {
-                        const f32x4 r0 = *(const f32x4*)((const float*)p.R + ro);
-                        const f32x4 r1 = *(const f32x4*)((const float*)p.R + ro + 4);
+                        const f32x4 r0 = __builtin_bit_cast(f32x4, rq[0]);
+                        const f32x4 r1 = __builtin_bit_cast(f32x4, rq[1]);
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             v[e] += r0[e];
@@ -218,7 +244,7 @@ __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x
                 }
             }
         }
-        __syncthreads();
+        asm volatile("" ::: "memory");
     }
 }
 

@@ -47,6 +47,13 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
 bool conv_gemm_big_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_big(const ConvGemmParams& p, Act out_type, Act compute,
                                 hipStream_t stream);
+// Other schedules of the 256x256 tile (same eligibility, tile 256 only):
+// persistent grid (conv_gemm_persist.hip) and wave-group ping-pong (conv_gemm_pp.hip).
+// big_schedule(): VP3D_GEMM=big|persist|pp -> 0|1|2.
+int big_schedule();
+hipError_t launch_conv_gemm_persist(const ConvGemmParams& p, Act out_type, Act compute,
+                                    hipStream_t stream);
+hipError_t launch_conv_gemm_pp(const ConvGemmParams& p, Act out_type, Act compute, hipStream_t stream);
 
 // Tile geometry the packer must pad to (rows of W to kPadN, K to kPadK).
 constexpr int kPadN = 256;

@@ -1,18 +1,24 @@
 #!/bin/bash
-# One GPU session: parity tests, then benches, then a rocprofv3 kernel-trace of the bench.
-# Usage (on the GPU box, from the repo root): bash tools/gpu_round.sh TAG [bench args...]
+# One GPU session: parity tests, the four bench configurations, and a rocprofv3
+# kernel trace of the headline bench.  Usage: bash tools/gpu_round.sh TAG
 set -o pipefail
-TAG=${1:-run}; shift
+TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -m pytest tests -m gpu -q -s -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?
-echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.log
+echo "pytest rc=$rc"; grep -E "passed|failed" $OUT/pytest_gpu.log | tail -2
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 "$@" > $OUT/bench_bf16.log 2>&1 || exit $?
-tail -1 $OUT/bench_bf16.log
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --dtype fp32 --cpu-seconds 0 "$@" > $OUT/bench_fp32.log 2>&1 || exit $?
-tail -1 $OUT/bench_fp32.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-seconds 0 "$@" > $OUT/prof.log 2>&1 || exit $?
-find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'cut -c1-200 {} | head -12'
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/bench_bf16.log 2>&1 || exit $?
+echo "bf16:   $(python tools/bench_brief.py $OUT/bench_bf16.log)"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --dtype fp16 --cpu-seconds 0 > $OUT/bench_fp16.log 2>&1 || exit $?
+echo "fp16:   $(python tools/bench_brief.py $OUT/bench_fp16.log)"
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --dtype fp32 --cpu-seconds 0 > $OUT/bench_fp32.log 2>&1 || exit $?
+echo "fp32:   $(python tools/bench_brief.py $OUT/bench_fp32.log)"
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --traj --cpu-seconds 0 > $OUT/bench_traj.log 2>&1 || exit $?
+echo "traj:   $(python tools/bench_brief.py $OUT/bench_traj.log)"
+timeout -k 10 300 python bench.py --stream --dtype fp16 --steps 4096 --warmup 128 --cpu-seconds 5 > $OUT/bench_stream.log 2>&1 || exit $?
+echo "stream: $(tail -1 $OUT/bench_stream.log | cut -c1-400)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-seconds 0 > $OUT/prof.log 2>&1 || exit $?
+echo "prof ok"
