@@ -55,6 +55,11 @@ hipError_t launch_conv_gemm_persist(const ConvGemmParams& p, Act out_type, Act c
                                     hipStream_t stream);
 hipError_t launch_conv_gemm_pp(const ConvGemmParams& p, Act out_type, Act compute, hipStream_t stream);
 
+// Expand convolution, 16-bit compute (expand_gemm.hip): reads the f32 input rows
+// directly (no packed copy), 256 rows x all channels per workgroup.
+bool expand_gemm_eligible(const ConvGemmParams& p, Act out_type, Act compute);
+hipError_t launch_expand_gemm(const ConvGemmParams& p, Act compute, hipStream_t stream);
+
 // Tile geometry the packer must pad to (rows of W to kPadN, K to kPadK).
 constexpr int kPadN = 256;
 constexpr int kPadK = 64;

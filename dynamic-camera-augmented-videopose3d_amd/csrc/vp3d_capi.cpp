@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -427,6 +428,15 @@ int vp3d_reserve(vp3d_handle* h, int B, int T, int dtype) {
     return ensure_ws(h, B, T, dtype);
 }
 
+// VP3D_EXPAND=pack selects the older pack-rows + generic GEMM expand path (A/B runs)
+static bool expand_gemm_env() {
+    static const bool on = [] {
+        const char* e = getenv("VP3D_EXPAND");
+        return !(e && !strcmp(e, "pack"));
+    }();
+    return on;
+}
+
 int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream) {
     if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
     if (!x || !y) return fail(VP3D_ERR_ARG, "x / y is NULL");
@@ -509,7 +519,14 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
             hipEventRecord(pe.a, s);
         }
         Act a_type = first ? Act::F32 : act;
-        if (first && act != Act::F32) {
+        const Act o_type = last ? Act::F32 : act;
+        hipError_t e = hipSuccess;
+        bool launched = false;
+        if (first && act != Act::F32 && expand_gemm_env() && expand_gemm_eligible(p, o_type, act)) {
+            // 16-bit expand conv straight from the f32 input rows (expand_gemm.hip)
+            e = launch_expand_gemm(p, act, s);
+            launched = true;
+        } else if (first && act != Act::F32) {
             // 16-bit path: pack the f32 input rows of the expand conv into zero-padded
             // 16-bit GEMM rows (one launch) so the conv runs on the tap-aligned kernel
             void* packed = base + 3 * buf_elems * es;
@@ -525,9 +542,7 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
             p.dil = 1;
             a_type = act;
         }
-        const Act o_type = last ? Act::F32 : act;
-
-        hipError_t e = launch_conv_gemm(p, a_type, o_type, act, s);
+        if (!launched) e = launch_conv_gemm(p, a_type, o_type, act, s);
         if (e != hipSuccess)
             return fail(VP3D_ERR_HIP, std::string("conv layer ") + std::to_string(li) + ": " +
                                           hipGetErrorString(e));

@@ -37,7 +37,7 @@ def main():
     print("| kernel | grid | layer | " + " | ".join(counters) + " |")
     print("|---|---|---|" + "---|" * len(counters))
     for (k, g), cs in sorted(vals.items(), key=lambda kv: -kv[0][1]):
-        if not k.startswith("conv_gemm") and "stream" not in k and "pack" not in k:
+        if not k.startswith("conv_gemm") and not any(s in k for s in ("stream", "pack", "expand")):
             continue
         row = []
         for c in counters:

@@ -1,0 +1,26 @@
+"""Calibration (tool, not product): hipBLASLt bf16 GEMM rate (torch.matmul) on the
+lifter's layer shapes at B = 8192 windows, for comparison with the conv-GEMM kernels."""
+import torch
+
+shapes = {  # name: (M, N, K)
+    "expand": (8192 * 81, 1024, 128),
+    "block1_k3": (8192 * 27, 1024, 3072),
+    "block1_1x1": (8192 * 27, 1024, 1024),
+    "block2_k3": (8192 * 9, 1024, 3072),
+    "block3_k3": (8192 * 3, 1024, 3072),
+}
+for name, (M, N, K) in shapes.items():
+    a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+    for _ in range(3):
+        torch.matmul(a, w.t())
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 10
+    e0.record()
+    for _ in range(n):
+        torch.matmul(a, w.t())
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    print(f"{name:12s} M={M:7d} N={N} K={K:5d}  {ms:.4f} ms  {2 * M * N * K / ms / 1e9:.1f} TFLOP/s", flush=True)
