@@ -336,6 +336,7 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     }
     if (a_type != Act::F32 && a_type != compute) return hipErrorInvalidValue;
     if (out_type != Act::F32 && out_type != compute) return hipErrorInvalidValue;
+    if (conv_gemm_tp_eligible(p, a_type, out_type, compute)) return launch_conv_gemm_tp(p, compute, stream);
     if (conv_gemm_big_eligible(p, a_type, out_type, compute))
         switch (big_schedule()) {
             case 1: return launch_conv_gemm_persist(p, out_type, compute, stream);

@@ -55,6 +55,12 @@ hipError_t launch_conv_gemm_persist(const ConvGemmParams& p, Act out_type, Act c
                                     hipStream_t stream);
 hipError_t launch_conv_gemm_pp(const ConvGemmParams& p, Act out_type, Act compute, hipStream_t stream);
 
+// Persistent transposed-MFMA 256x256 kernel with register-direct epilogue
+// (conv_gemm_tp.hip): default for the large layers with 16-bit output
+// (VP3D_GEMM=big|persist|pp selects the older schedules for A/B runs).
+bool conv_gemm_tp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
+hipError_t launch_conv_gemm_tp(const ConvGemmParams& p, Act compute, hipStream_t stream);
+
 // Expand convolution, 16-bit compute (expand_gemm.hip): reads the f32 input rows
 // directly (no packed copy), 256 rows x all channels per workgroup.
 bool expand_gemm_eligible(const ConvGemmParams& p, Act out_type, Act compute);

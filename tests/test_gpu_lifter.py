@@ -63,6 +63,22 @@ def test_opt1f_243_h16(dtype):
     _check(y, ref, gt, dtype)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_opt1f_243_h16_large_batch(dtype):
+    # B = 2050 windows: the block-1/2 layers (M = 55,350 / 18,450 rows, the last
+    # 256-row tile partial) run on the persistent 256x256 kernel and the expand conv on
+    # the fused expand kernel -- the kernels the headline bench times
+    y, ref, gt = _run(True, 2050, 243, dtype=dtype)
+    _check(y, ref, gt, dtype)
+
+
+def test_dilated_long_seq_bf16():
+    # one long sequence: every block layer has >= 256 output tiles, so the dilated
+    # taps (row offsets 0, d, 2d) and the residual slice run on the persistent kernel
+    y, ref, gt = _run(False, 1, 20242, dtype="bf16")
+    _check(y, ref, gt, "bf16")
+
+
 @pytest.mark.parametrize("causal", [False, True])
 def test_dilated_seq_243_fp32(causal):
     y, ref, gt = _run(False, 1, 600, causal=causal)

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Per-layer HBM traffic of the lifter forward from rocprofv3 PMC passes.
+
+    python tools/traffic.py gpurun_out/TAG [--batch 8192] [--dtype bf16] [--out profiles/traffic_bf16_b8192.json]
+
+Reads the FETCH_SIZE and WRITE_SIZE passes (`tools/pmc_pass.sh TAG FETCH_SIZE WRITE_SIZE`
+over a `bench.py` run), orders the dispatches by Dispatch_Id and splits them into
+forwards: a forward starts at the expand-conv dispatch of the bench batch (grid =
+ceil(B*81/256) workgroups of 256 threads for the fused expand kernel, or the
+pack-rows kernel of the older path) and is followed by the 9 conv-GEMM dispatches
+of blocks 1-4 and the shrink, in layer order.
+
+Units and corrections (MI355X_MICROARCH.md, "HBM"): FETCH_SIZE and WRITE_SIZE
+are KiB; on gfx950 FETCH_SIZE tallies each 128-byte read request as 64 bytes, so
+the read side is doubled.  WRITE_SIZE is exact for 16-byte-per-lane stores.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+LAYERS = ["expand", "block1_k3", "block1_1x1", "block2_k3", "block2_1x1", "block3_k3",
+          "block3_1x1", "block4_k3", "block4_1x1", "shrink"]
+
+
+def read_counter(d, name):
+    rows = {}
+    for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r["Counter_Name"] != name:
+                    continue
+                rows[int(r["Dispatch_Id"])] = (r["Kernel_Name"], int(r["Grid_Size"]), float(r["Counter_Value"]))
+    return rows
+
+
+def forwards(rows, B):
+    """Yield lists of (layer, value) per forward of batch B."""
+    ids = sorted(rows)
+    expand_grid = ((B * 81 + 255) // 256) * 256
+    i = 0
+    while i < len(ids):
+        name, grid, _ = rows[ids[i]]
+        start = ("expand_gemm" in name and grid == expand_grid)
+        if not start:
+            i += 1
+            continue
+        seq = [("expand", rows[ids[i]][2])]
+        j = i + 1
+        while j < len(ids) and len(seq) < len(LAYERS):
+            n2, g2, v2 = rows[ids[j]]
+            if "conv_gemm" in n2:
+                seq.append((LAYERS[len(seq)], v2))
+            j += 1
+        if len(seq) == len(LAYERS):
+            yield seq
+        i = j
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dominant", default="block1_k3")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    acc = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+    for c in acc:
+        for seq in forwards(read_counter(a.dir, c), a.batch):
+            for layer, v in seq:
+                acc[c][layer].append(v)
+    per_layer = {}
+    for layer in LAYERS:
+        f, w = acc["FETCH_SIZE"].get(layer), acc["WRITE_SIZE"].get(layer)
+        if not f or not w:
+            continue
+        rd = 2.0 * 1024.0 * sum(f) / len(f)
+        wr = 1024.0 * sum(w) / len(w)
+        per_layer[layer] = {"read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
+                            "launches": min(len(f), len(w))}
+    out = {"batch": a.batch, "dtype": a.dtype, "dominant": a.dominant,
+           "hbm_bytes_per_launch": per_layer.get(a.dominant, {}).get("hbm_bytes"),
+           "per_layer": per_layer,
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in {a.dir}; "
+                     "FETCH_SIZE x 2 (gfx950 128-B requests tallied as 64 B), KiB -> B"}
+    s = json.dumps(out, indent=1)
+    print(s)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
