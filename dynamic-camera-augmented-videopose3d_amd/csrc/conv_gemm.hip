@@ -22,6 +22,9 @@
 //    4 consecutive k of its row in one ds_read_b128 and feeds them to 4
 //    successive MFMAs (k = 4*(l>>4) + s); A and B use the same k permutation,
 //    so the dot product is unchanged.
+#include <cstdlib>
+#include <cstring>
+
 #include "gemm_common.h"
 
 namespace vp3d {
@@ -312,6 +315,24 @@ hipError_t launch_f32(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t
     return hipGetLastError();
 }
 
+// Which 256x256 kernel a large layer runs on (VP3D_GEMM overrides for A/B runs):
+//   default: the ping-pong kernel (conv_gemm_8p.hip) for layers without a residual
+//   (the k-tap convs: 1.20 vs 1.22 ms on block 1 at B = 8192), the LDS-ring kernel
+//   (conv_gemm_big.hip) for the 1x1 convs with a residual (0.56 vs 0.58 ms);
+//   VP3D_GEMM=8p -> 8p everywhere; big / persist / pp / tp -> that schedule everywhere.
+int gemm_8p_mode() {
+    static const int v = [] {
+        const char* e = getenv("VP3D_GEMM");
+        if (!e) return 1;
+        return strcmp(e, "8p") == 0 ? 2 : 0;
+    }();
+    return v;
+}
+bool gemm_8p_env(const ConvGemmParams& p) {
+    const int m = gemm_8p_mode();
+    return m == 2 || (m == 1 && p.R == nullptr);
+}
+
 bool aligned(const void* ptr, uintptr_t a) { return (reinterpret_cast<uintptr_t>(ptr) & (a - 1)) == 0; }
 
 }  // namespace
@@ -337,6 +358,9 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     if (a_type != Act::F32 && a_type != compute) return hipErrorInvalidValue;
     if (out_type != Act::F32 && out_type != compute) return hipErrorInvalidValue;
     if (conv_gemm_tp_eligible(p, a_type, out_type, compute)) return launch_conv_gemm_tp(p, compute, stream);
+    if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
+        conv_gemm_8p_eligible(p, a_type, out_type, compute))
+        return launch_conv_gemm_8p(p, compute, stream);
     if (conv_gemm_big_eligible(p, a_type, out_type, compute))
         switch (big_schedule()) {
             case 1: return launch_conv_gemm_persist(p, out_type, compute, stream);

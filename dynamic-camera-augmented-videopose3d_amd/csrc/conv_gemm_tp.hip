@@ -57,10 +57,6 @@ __device__ __forceinline__ void vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-
 template <typename CT>
 __global__ __launch_bounds__(512, 1) void conv_gemm_tp(ConvGemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[TRING + 2 * TMAXN * 4];
@@ -173,86 +169,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_tp(ConvGemmParams p) {
 
     // ---- epilogue: exactly TEPI_VMEM vector-memory instructions per wave (stores)
     // plus, with a residual, 16 loads that are waited for inside ----
-    const int grp = lane >> 4;
-    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));  // lane's 8-channel group within 32
     const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.ldy * sizeof(CT)));
     auto epilogue = [&](int j) {
         const int t = r + j * G;
         const int tm = t / ntn;
-        const int mw = tm * TM + wr * 128;
-        const int nw = (t - tm * ntn) * TN + wc * 64;
-        float sc[2][8], sh[2][8];
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-            const int n = nw + 32 * jp + c0;
-            const f32x4 s0 = *(const f32x4*)&s_scale[n], s1 = *(const f32x4*)&s_scale[n + 4];
-            const f32x4 h0 = *(const f32x4*)&s_shift[n], h1 = *(const f32x4*)&s_shift[n + 4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                sc[jp][e] = s0[e];
-                sc[jp][e + 4] = s1[e];
-                sh[jp][e] = h0[e];
-                sh[jp][e + 4] = h1[e];
-            }
-        }
-        // residual rows one row block ahead: clamped row index (always a valid
-        // address; values of rows past M are never stored).  Issue order per block
-        // i: res(i+1), [wait res(i)], stores(i) -> younger than res(i) at its wait:
-        // res(i+1) and stores(i-1), 2 instructions each.
-        const bool has_r = p.R != nullptr;
-        u32x4 res[2][2];
-        auto load_res = [&](int i, u32x4 (&rr)[2]) {
-            int m = mw + i * 16 + (lane & 15);
-            m = m < p.M ? m : p.M - 1;
-            const CT* rp = (const CT*)p.R + (int64_t)res_row(p, m) * p.ldr + nw + c0;
-            rr[0] = *(const u32x4*)rp;
-            rr[1] = *(const u32x4*)(rp + 32);
-        };
-        if (has_r) load_res(0, res[0]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int m = mw + i * 16 + (lane & 15);
-            if (has_r) {
-                if (i + 1 < 8) load_res(i + 1, res[(i + 1) & 1]);
-                if (i == 0)
-                    vm_wait<2>();
-                else if (i + 1 < 8)
-                    vm_wait<4>();
-                else
-                    vm_wait<2>();
-            }
-#pragma unroll
-            for (int jp = 0; jp < 2; ++jp) {
-                f32x4 X = acc[i][2 * jp], Y = acc[i][2 * jp + 1];
-                float v[8];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, X[d]),
-                                                                     __builtin_bit_cast(unsigned, Y[d]),
-                                                                     false, false);
-                    v[d] = __builtin_bit_cast(float, (unsigned)sw[0]);
-                    v[d + 4] = __builtin_bit_cast(float, (unsigned)sw[1]);
-                }
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    v[e] = __fadd_rn(__fmul_rn(v[e], sc[jp][e]), sh[jp][e]);
-                    if (p.relu) v[e] = v[e] > 0.f ? v[e] : 0.f;
-                }
-                typedef CT ct8 __attribute__((ext_vector_type(8)));
-                if (has_r) {
-                    const ct8 r8 = __builtin_bit_cast(ct8, res[i & 1][jp]);
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
-                }
-                ct8 o;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) o[e] = (CT)v[e];
-                // rows past M: byte offset beyond the buffer's range, dropped by hardware
-                const uint32_t yo = m < p.M ? (uint32_t)(((size_t)m * p.ldy + nw + 32 * jp + c0) * sizeof(CT))
-                                            : 0xFFFFFFF0u;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), y_rsrc, yo, 0, 0);
-            }
-        }
+        epilogue_tp<CT, 8>(p, acc, tm * TM + wr * 128, (t - tm * ntn) * TN + wc * 64, lane, s_scale, s_shift,
+                           y_rsrc);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -349,7 +271,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_tp(ConvGemmParams p) {
 bool conv_gemm_tp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
     static const bool on = [] {
         const char* e = getenv("VP3D_GEMM");
-        return !(e && strcmp(e, "tp") != 0);
+        return e && strcmp(e, "tp") == 0;
     }();
     if (!on) return false;
     if (compute == Act::F32 || a_type != compute || out_type != compute) return false;

@@ -248,5 +248,120 @@ __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x
     }
 }
 
+// ---------------------------------------------------------------------------
+// Register-direct epilogue for the transposed MFMA orientation (D = W . A^T):
+// acc[i][j] of a lane holds output channels nw + 16j + 4(lane>>4) + (0..3) of row
+// mw + 16i + (lane & 15).  BatchNorm affine + ReLU run in that layout (scale/shift
+// from LDS), then one v_permlane16_swap per value pair gives each lane 8
+// consecutive channels (nw + 32jp + c0 + 0..7, c0 = 0/16/8/24 for lane>>4 = 0..3),
+// the residual is added in f32, converted once, and stored as 16 bytes: every
+// store instruction writes 16 rows x 64 B.  Stores (and residual loads) use a
+// buffer resource so rows past M are dropped by the range check, not a branch:
+// every wave issues exactly 2*MI stores, the count the callers' vmcnt waits use.
+// With a residual the loads run one row block ahead of the stores and are waited
+// for here (vmcnt(2)/(4): older vector-memory operations are waited for too).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Residual rows of a wave's (16*MI) x 64 output block, loaded to registers ahead of
+// the epilogue (2*MI 16-byte loads, lane layout of epilogue_tp): callers that have the
+// VGPRs issue them during the last K-steps so the epilogue never waits on them.
+template <typename CT, int MI>
+__device__ __forceinline__ void load_residual_tp(const ConvGemmParams& p, u32x4 (&res)[MI][2], int mw, int nw,
+                                                 int lane) {
+    const int grp = lane >> 4;
+    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        int m = mw + i * 16 + (lane & 15);
+        m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
+        const CT* rp = (const CT*)p.R + (int64_t)res_row(p, m) * p.ldr + nw + c0;
+        res[i][0] = *(const u32x4*)rp;
+        res[i][1] = *(const u32x4*)(rp + 32);
+    }
+}
+
+// PRE: the residual is already in `pre` (load_residual_tp, waited for by the caller).
+template <typename CT, int MI, bool PRE = false>
+__device__ __forceinline__ void epilogue_tp(const ConvGemmParams& p, f32x4 (&acc)[MI][4], int mw, int nw,
+                                            int lane, const float* s_scale, const float* s_shift,
+                                            __amdgpu_buffer_rsrc_t y_rsrc, const u32x4 (*pre)[2] = nullptr) {
+    const int grp = lane >> 4;
+    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+    float sc[4][4], sh[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = nw + 16 * j + 4 * grp;
+        const f32x4 s4 = *(const f32x4*)&s_scale[n];
+        const f32x4 h4 = *(const f32x4*)&s_shift[n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            sc[j][q] = s4[q];
+            sh[j][q] = h4[q];
+        }
+    }
+    const bool has_r = p.R != nullptr;
+    u32x4 res[2][2];
+    auto load_res = [&](int i, u32x4 (&rr)[2]) {
+        int m = mw + i * 16 + (lane & 15);
+        m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
+        const CT* rp = (const CT*)p.R + (int64_t)res_row(p, m) * p.ldr + nw + c0;
+        rr[0] = *(const u32x4*)rp;
+        rr[1] = *(const u32x4*)(rp + 32);
+    };
+    if (has_r && !PRE) load_res(0, res[0]);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int m = mw + i * 16 + (lane & 15);
+        if (has_r && !PRE) {
+            // issue order per block: res(i+1), [wait res(i)], stores(i)
+            if (i + 1 < MI) load_res(i + 1, res[(i + 1) & 1]);
+            if (i == 0)
+                vm_wait_n<2>();
+            else if (i + 1 < MI)
+                vm_wait_n<4>();
+            else
+                vm_wait_n<2>();
+        }
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+            float v[8];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                float x = __fadd_rn(__fmul_rn(acc[i][2 * jp][d], sc[2 * jp][d]), sh[2 * jp][d]);
+                float y = __fadd_rn(__fmul_rn(acc[i][2 * jp + 1][d], sc[2 * jp + 1][d]), sh[2 * jp + 1][d]);
+                if (p.relu) {
+                    x = x > 0.f ? x : 0.f;
+                    y = y > 0.f ? y : 0.f;
+                }
+                // odd 16-lane rows of x <-> even rows of y.  Inline asm: hipcc 7.2 folds
+                // repeated __builtin_amdgcn_permlane16_swap calls on different operands
+                // into one (miscompile); x, y were just written by VALU -> 2 wait states
+                asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+                v[d] = x;
+                v[d + 4] = y;
+            }
+            typedef CT ct8 __attribute__((ext_vector_type(8)));
+            if (has_r) {
+                const ct8 r8 = __builtin_bit_cast(ct8, PRE ? pre[i][jp] : res[i & 1][jp]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
+            }
+            ct8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (CT)v[e];
+            const uint32_t yo = m < p.M ? (uint32_t)(((size_t)m * p.ldy + nw + 32 * jp + c0) * sizeof(CT))
+                                        : 0xFFFFFFF0u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), y_rsrc, yo, 0, 0);
+        }
+    }
+}
+
 }  // namespace gemm
 }  // namespace vp3d

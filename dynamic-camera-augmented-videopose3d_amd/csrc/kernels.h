@@ -61,6 +61,10 @@ hipError_t launch_conv_gemm_pp(const ConvGemmParams& p, Act out_type, Act comput
 bool conv_gemm_tp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_tp(const ConvGemmParams& p, Act compute, hipStream_t stream);
 
+// Wave-group ping-pong 256x256 kernel with register-direct epilogue (conv_gemm_8p.hip).
+bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
+hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream);
+
 // Expand convolution, 16-bit compute (expand_gemm.hip): reads the f32 input rows
 // directly (no packed copy), 256 rows x all channels per workgroup.
 bool expand_gemm_eligible(const ConvGemmParams& p, Act out_type, Act compute);
