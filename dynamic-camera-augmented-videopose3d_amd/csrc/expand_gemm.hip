@@ -27,6 +27,8 @@
 //     kernel's speed: with 8-byte stores straight from the accumulators (16 rows
 //     x 32 B per instruction) the TA was busy 80 % of the kernel at ~120 cycles
 //     per store instruction (rocprofv3 TA_BUSY / TA_FLAT_WRITE_WAVEFRONTS).
+#include <cstdlib>
+
 #include "gemm_common.h"
 
 namespace vp3d {
@@ -34,9 +36,7 @@ namespace {
 
 using namespace gemm;
 
-constexpr int kExpRowsPerWave = 64;  // 4 row blocks of 16
 constexpr int kExpWaves = 4;
-constexpr int kExpRows = kExpRowsPerWave * kExpWaves;  // 256 rows per workgroup
 constexpr int kExpChunkN = 64;                          // output channels per chunk
 constexpr int kExpMaxN = 1024;
 
@@ -45,8 +45,11 @@ constexpr int kExpMaxN = 1024;
 // reads (row l&15 of a 16-row block, chunk l>>4) are bank-conflict free.
 __device__ __forceinline__ int exp_swz(int r, int c) { return r * 4 + ((c + 2 * ((r >> 2) & 3)) & 3); }
 
-template <typename CT, int NKS>
-__global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p) {
+// RB = row blocks of 16 per wave (64 * RB rows per workgroup).
+template <typename CT, int NKS, int RB>
+__global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p) {
+    constexpr int kExpRowsPerWave = 16 * RB;
+    constexpr int kExpRows = kExpRowsPerWave * kExpWaves;
     constexpr int SLAB = kExpChunkN * 4;       // 16-byte units per k-step slab
     constexpr int CHUNK_U = NKS * SLAB;        // 16-byte units per weight chunk
     __shared__ __attribute__((aligned(16))) u32x4 wbuf[2][CHUNK_U];
@@ -81,9 +84,9 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p) {
 
     // ---- A fragments: row (l & 15) of each 16-row block, k = 32*ks + 8*(l>>4) .. +7 ----
     const float* X = (const float*)p.A;
-    u32x4 af[4][NKS];
+    u32x4 af[RB][NKS];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
+    for (int rb = 0; rb < RB; ++rb) {
         int m = m_wave + rb * 16 + (lane & 15);
         m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
         const float* row = X + (int64_t)src_row(p, m) * p.lda;
@@ -113,9 +116,9 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p) {
     CT* Y = (CT*)p.Y;
     for (int ch = 0; ch < nchunks; ++ch) {
         const int buf = ch & 1;
-        f32x4 acc[4][4];
+        f32x4 acc[RB][4];
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+        for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) wf[j] = wbuf[buf][ks * SLAB + j * 64 + frag_off];
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
+            for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[rb][j] = mfma16<CT>(wf[j], af[rb][ks], acc[rb][j]);
         }
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p) {
             const f32x4 sc = *(const f32x4*)&s_scale[n0 + nl];
             const f32x4 sh = *(const f32x4*)&s_shift[n0 + nl];
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb) {
+            for (int rb = 0; rb < RB; ++rb) {
                 ct4 o;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p) {
         asm volatile("" ::: "memory");
         // 8 lanes per row, 8 rows per instruction: whole 128-byte lines
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < 2 * RB; ++q) {
             const int row = q * 8 + (lane >> 3);
             const int c16 = lane & 7;
             const u32x4 v = stage[row * 8 + (c16 ^ (row & 7))];
@@ -172,18 +175,38 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p) {
     }
 }
 
-template <typename CT>
-hipError_t launch_t(const ConvGemmParams& p, int nks, hipStream_t s) {
-    const dim3 grid((p.M + kExpRows - 1) / kExpRows);
+template <typename CT, int RB>
+hipError_t launch_rb(const ConvGemmParams& p, int nks, hipStream_t s) {
+    const dim3 grid((p.M + 64 * RB - 1) / (64 * RB));
     switch (nks) {
-        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1>), grid, dim3(256), 0, s, p); break;
-        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2>), grid, dim3(256), 0, s, p); break;
-        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3>), grid, dim3(256), 0, s, p); break;
-        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4>), grid, dim3(256), 0, s, p); break;
-        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5>), grid, dim3(256), 0, s, p); break;
+        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB>), grid, dim3(256), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB>), grid, dim3(256), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB>), grid, dim3(256), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB>), grid, dim3(256), 0, s, p); break;
+        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB>), grid, dim3(256), 0, s, p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+// Row blocks of 16 per wave (VP3D_EXPAND_RB = 1, 2 or 4): fewer rows per wave, fewer
+// VGPRs and less LDS per workgroup, more resident waves to hide store / input latency.
+int expand_rb() {
+    static const int v = [] {
+        const char* e = getenv("VP3D_EXPAND_RB");
+        const int r = e ? atoi(e) : 4;  // measured at B = 8192: 4 -> 0.370, 2 -> 0.406, 1 -> 0.442 ms
+        return (r == 1 || r == 2 || r == 4) ? r : 4;
+    }();
+    return v;
+}
+
+template <typename CT>
+hipError_t launch_t(const ConvGemmParams& p, int nks, hipStream_t s) {
+    switch (expand_rb()) {
+        case 1: return launch_rb<CT, 1>(p, nks, s);
+        case 2: return launch_rb<CT, 2>(p, nks, s);
+        default: return launch_rb<CT, 4>(p, nks, s);
+    }
 }
 
 }  // namespace

@@ -1,12 +1,14 @@
 #!/bin/bash
-# One GPU session: parity tests, the four bench configurations, and a rocprofv3
-# kernel trace of the headline bench.  Usage: bash tools/gpu_round.sh TAG
+# One GPU session: parity tests, the bench configurations, a rocprofv3 kernel trace
+# of the headline bench and the FETCH_SIZE / WRITE_SIZE PMC passes (separate runs,
+# counters only) that tools/traffic.py turns into per-layer HBM bytes.
+# Usage: bash tools/gpu_round.sh TAG
 set -o pipefail
 TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -q -s -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed" $OUT/pytest_gpu.log | tail -2
 if [ $rc -gt 1 ]; then exit $rc; fi
@@ -19,6 +21,10 @@ echo "fp32:   $(python tools/bench_brief.py $OUT/bench_fp32.log)"
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --traj --cpu-seconds 0 > $OUT/bench_traj.log 2>&1 || exit $?
 echo "traj:   $(python tools/bench_brief.py $OUT/bench_traj.log)"
 timeout -k 10 300 python bench.py --stream --dtype fp16 --steps 4096 --warmup 128 --cpu-seconds 5 > $OUT/bench_stream.log 2>&1 || exit $?
-echo "stream: $(tail -1 $OUT/bench_stream.log | cut -c1-400)"
+echo "stream: $(tail -1 $OUT/bench_stream.log | cut -c1-300)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --cpu-seconds 0 > $OUT/prof.log 2>&1 || exit $?
 echo "prof ok"
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$C -o run -- python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --parity-windows 4 > $OUT/pmc_$C.log 2>&1 || exit $?
+  echo "pmc $C ok"
+done

@@ -60,5 +60,55 @@ def main():
               f"{sum(ds) / len(ds):.1f} | {ds_sorted[0]:.1f} | {ds_sorted[-1]:.1f} |")
 
 
+def per_layer(trace, B):
+    """Per-layer durations by dispatch order: a forward of batch B starts at its expand
+    dispatch (fused expand kernel, grid = ceil(B*81/256)*256 threads) and is followed by
+    the 9 conv-GEMM dispatches of blocks 1-4 and the shrink."""
+    layers = ["expand", "block1_k3", "block1_1x1", "block2_k3", "block2_1x1", "block3_k3",
+              "block3_1x1", "block4_k3", "block4_1x1", "shrink"]
+    rows = []
+    with open(trace) as f:
+        for r in csv.DictReader(f):
+            if r.get("Kind", "KERNEL_DISPATCH") != "KERNEL_DISPATCH":
+                continue
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], int(r["Grid_Size_X"]),
+                         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    rows.sort()
+    eg = ((B * 81 + 255) // 256) * 256
+    agg = defaultdict(list)
+    names = {}
+    i = 0
+    while i < len(rows):
+        if "expand_gemm" in rows[i][1] and rows[i][2] == eg:
+            seq = [rows[i]]
+            j = i + 1
+            while j < len(rows) and len(seq) < len(layers):
+                if "conv_gemm" in rows[j][1]:
+                    seq.append(rows[j])
+                j += 1
+            if len(seq) == len(layers):
+                for name, r in zip(layers, seq):
+                    agg[name].append(r[3])
+                    names[name] = short(r[1])
+            i = j
+        else:
+            i += 1
+    print()
+    print(f"Per layer (forwards of B = {B}, by dispatch order):")
+    print()
+    print("| layer | kernel | calls | avg us | min us | max us |")
+    print("|---|---|---|---|---|---|")
+    for name in layers:
+        ds = sorted(agg.get(name, []))
+        if ds:
+            print(f"| {name} | {names[name]} | {len(ds)} | {sum(ds) / len(ds):.1f} | {ds[0]:.1f} | {ds[-1]:.1f} |")
+
+
 if __name__ == "__main__":
     main()
+    import sys
+    if len(sys.argv) > 1:
+        B = 8192
+        if "--batch" in sys.argv:
+            B = int(sys.argv[sys.argv.index("--batch") + 1])
+        per_layer(sys.argv[1], B)
