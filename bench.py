@@ -205,7 +205,7 @@ def main():
     if args.traj:
         from vp3d_amd.pipeline import SyntheticTrajectoryBatcher
         pipe = SyntheticTrajectoryBatcher(B, RF, seed=1000 + rank, device=dev)
-        x = pipe.next_batch()
+        x = None
     else:
         x = synth_windows(B, RF, jin, 1000 + rank, dev)
     lifter = model.native_lifter(dev)
@@ -215,9 +215,15 @@ def main():
     last_in = [x]
 
     def step():
-        xin = pipe.next_batch() if pipe is not None else x
-        lifter.forward(xin, args.dtype, out=y)
-        last_in[0] = xin
+        if pipe is not None:
+            # config 3: K.E of every frame + window gather + camera concat + forward,
+            # the gather fused into the expand conv's operand loads
+            pairs = pipe.next_pairs()
+            lifter.forward_windows(pipe.seqs, pairs, RF, pipe.pad, concat_cams=True, dtype=args.dtype,
+                                   out=y)
+            last_in[0] = pairs
+        else:
+            lifter.forward(x, args.dtype, out=y)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -263,7 +269,8 @@ def main():
         # P windows, plus the fp32 parity path on the same windows
         P = min(args.parity_windows, B)
         idx = torch.cat([torch.arange(P // 2), torch.arange(B - (P - P // 2), B)]).to(dev)
-        xs = last_in[0][idx].contiguous()
+        xfull = pipe.gather(last_in[0]) if pipe is not None else last_in[0]
+        xs = xfull[idx].contiguous()
         y_fast = y[idx].cpu().numpy()
         with torch.no_grad():
             model.set_compute_dtype("fp32")

@@ -46,8 +46,11 @@ constexpr int kExpMaxN = 1024;
 __device__ __forceinline__ int exp_swz(int r, int c) { return r * 4 + ((c + 2 * ((r >> 2) & 3)) & 3); }
 
 // RB = row blocks of 16 per wave (64 * RB rows per workgroup).
-template <typename CT, int NKS, int RB>
-__global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p) {
+// GATHER: the input rows are not a (B, T, Cin) tensor but windows of device-resident
+// sequences, gathered here (GatherSrc, kernels.h): the ChunkedGenerator batch and the
+// camera concat fused into the operand loader.
+template <typename CT, int NKS, int RB, bool GATHER>
+__global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
     constexpr int kExpRowsPerWave = 16 * RB;
     constexpr int kExpRows = kExpRowsPerWave * kExpWaves;
     constexpr int SLAB = kExpChunkN * 4;       // 16-byte units per k-step slab
@@ -89,20 +92,53 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p) {
     for (int rb = 0; rb < RB; ++rb) {
         int m = m_wave + rb * 16 + (lane & 15);
         m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
-        const float* row = X + (int64_t)src_row(p, m) * p.lda;
+        if constexpr (!GATHER) {
+            const float* row = X + (int64_t)src_row(p, m) * p.lda;
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            const int k0 = ks * 32 + (lane >> 4) * 8;
-            float v[8];
+            for (int ks = 0; ks < NKS; ++ks) {
+                const int k0 = ks * 32 + (lane >> 4) * 8;
+                float v[8];
 #pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-                // K even: pairs are wholly in or out; out-of-range pairs read pair 0
-                const bool in = k0 + e < p.K;
-                const float2 t = *(const float2*)(row + (in ? k0 + e : 0));
-                v[e] = in ? t.x : 0.f;
-                v[e + 1] = in ? t.y : 0.f;
+                for (int e = 0; e < 8; e += 2) {
+                    // K even: pairs are wholly in or out; out-of-range pairs read pair 0
+                    const bool in = k0 + e < p.K;
+                    const float2 t = *(const float2*)(row + (in ? k0 + e : 0));
+                    v[e] = in ? t.x : 0.f;
+                    v[e + 1] = in ? t.y : 0.f;
+                }
+                af[rb][ks] = pack8<CT>(v);
             }
-            af[rb][ks] = pack8<CT>(v);
+        } else {
+            // window b starts at sequence frame start_b - lead; row t covers window frames
+            // t*stride + tap, tap < K / lda; frame j of the window is sequence frame
+            // clamp(start_b - lead + j, 0, len - 1) ('edge' padding, generators.py:92-100)
+            const int b = m / p.T_out;
+            const int t = m - b * p.T_out;
+            const int2 pr = *(const int2*)(g.pairs + 2 * b);
+            const int64_t off = g.seq_off[pr.x];
+            const int len = g.seq_len[pr.x];
+            const int f0 = pr.y - g.lead + t * p.stride;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const int k0 = ks * 32 + (lane >> 4) * 8;
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                    // lda, f2 and K even: a pair never straddles a tap or the kps|cams edge
+                    const int k = k0 + e;
+                    const bool in = k < p.K;
+                    const int tap = in ? k / p.lda : 0;
+                    const int c = in ? k - tap * p.lda : 0;
+                    int fr = f0 + tap;
+                    fr = fr < 0 ? 0 : (fr >= len ? len - 1 : fr);
+                    const int64_t gf = off + fr;
+                    const float* src = c < g.f2 ? g.kps + gf * g.f2 + c : g.cams + gf * 12 + (c - g.f2);
+                    const float2 tv = *(const float2*)src;
+                    v[e] = in ? tv.x : 0.f;
+                    v[e + 1] = in ? tv.y : 0.f;
+                }
+                af[rb][ks] = pack8<CT>(v);
+            }
         }
     }
 
@@ -175,15 +211,15 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p) {
     }
 }
 
-template <typename CT, int RB>
-hipError_t launch_rb(const ConvGemmParams& p, int nks, hipStream_t s) {
+template <typename CT, int RB, bool GATHER>
+hipError_t launch_rb(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     const dim3 grid((p.M + 64 * RB - 1) / (64 * RB));
     switch (nks) {
-        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB>), grid, dim3(256), 0, s, p); break;
-        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB>), grid, dim3(256), 0, s, p); break;
-        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB>), grid, dim3(256), 0, s, p); break;
-        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB>), grid, dim3(256), 0, s, p); break;
-        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB>), grid, dim3(256), 0, s, p); break;
+        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
+        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
+        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
+        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
+        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -200,12 +236,12 @@ int expand_rb() {
     return v;
 }
 
-template <typename CT>
-hipError_t launch_t(const ConvGemmParams& p, int nks, hipStream_t s) {
+template <typename CT, bool GATHER>
+hipError_t launch_t(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     switch (expand_rb()) {
-        case 1: return launch_rb<CT, 1>(p, nks, s);
-        case 2: return launch_rb<CT, 2>(p, nks, s);
-        default: return launch_rb<CT, 4>(p, nks, s);
+        case 1: return launch_rb<CT, 1, GATHER>(p, g, nks, s);
+        case 2: return launch_rb<CT, 2, GATHER>(p, g, nks, s);
+        default: return launch_rb<CT, 4, GATHER>(p, g, nks, s);
     }
 }
 
@@ -222,9 +258,24 @@ bool expand_gemm_eligible(const ConvGemmParams& p, Act out_type, Act compute) {
     return p.R == nullptr && p.M > 0;
 }
 
+bool expand_gather_eligible(const ConvGemmParams& p, const GatherSrc& g, Act out_type, Act compute) {
+    if (!expand_gemm_eligible(p, out_type, compute)) return false;
+    if (g.f2 % 2 || (reinterpret_cast<uintptr_t>(g.kps) & 7) || (g.cams && (reinterpret_cast<uintptr_t>(g.cams) & 7)))
+        return false;
+    return p.lda == g.f2 + (g.cams ? 12 : 0);
+}
+
 hipError_t launch_expand_gemm(const ConvGemmParams& p, Act compute, hipStream_t stream) {
     const int nks = (p.K + 31) / 32;
-    return compute == Act::BF16 ? launch_t<bf16>(p, nks, stream) : launch_t<f16>(p, nks, stream);
+    const GatherSrc none{};
+    return compute == Act::BF16 ? launch_t<bf16, false>(p, none, nks, stream)
+                                : launch_t<f16, false>(p, none, nks, stream);
+}
+
+hipError_t launch_expand_gemm_gather(const ConvGemmParams& p, const GatherSrc& g, Act compute,
+                                     hipStream_t stream) {
+    const int nks = (p.K + 31) / 32;
+    return compute == Act::BF16 ? launch_t<bf16, true>(p, g, nks, stream) : launch_t<f16, true>(p, g, nks, stream);
 }
 
 }  // namespace vp3d

@@ -65,10 +65,29 @@ hipError_t launch_conv_gemm_tp(const ConvGemmParams& p, Act compute, hipStream_t
 bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream);
 
+// Window source for a forward that gathers its input on the fly (vp3d_forward_windows):
+// the B windows are frames [start_b - lead, start_b - lead + window) of device-resident
+// sequences, edge-clamped per sequence (ChunkedGenerator, generators.py:92-137), each
+// frame = [kps (f2 floats) | cams (12 floats, K.E) if cams != nullptr]
+// (CamTransformer.py:187-190).  pairs: (B, 2) int32 (sequence, start).
+struct GatherSrc {
+    const float* kps = nullptr;
+    int f2 = 0;
+    const float* cams = nullptr;
+    const int64_t* seq_off = nullptr;
+    const int32_t* seq_len = nullptr;
+    const int32_t* pairs = nullptr;
+    int lead = 0;
+};
+
 // Expand convolution, 16-bit compute (expand_gemm.hip): reads the f32 input rows
-// directly (no packed copy), 256 rows x all channels per workgroup.
+// directly (no packed copy), 256 rows x all channels per workgroup; the gather form
+// reads the window frames straight from the sequences.
 bool expand_gemm_eligible(const ConvGemmParams& p, Act out_type, Act compute);
 hipError_t launch_expand_gemm(const ConvGemmParams& p, Act compute, hipStream_t stream);
+bool expand_gather_eligible(const ConvGemmParams& p, const GatherSrc& g, Act out_type, Act compute);
+hipError_t launch_expand_gemm_gather(const ConvGemmParams& p, const GatherSrc& g, Act compute,
+                                     hipStream_t stream);
 
 // Tile geometry the packer must pad to (rows of W to kPadN, K to kPadK).
 constexpr int kPadN = 256;

@@ -85,6 +85,9 @@ struct vp3d_handle {
     // activation workspace: three buffers of ws_elems elements of ws_esize bytes
     void* ws = nullptr;
     size_t ws_bytes = 0;
+    // window-gather scratch of vp3d_forward_windows when the fused expand path does not apply
+    float* gather_ws = nullptr;
+    size_t gather_bytes = 0;
     // profiling
     bool profiling = false;
     std::vector<ProfEvent> pending;
@@ -382,6 +385,7 @@ int vp3d_destroy(vp3d_handle* h) {
     hipSetDevice(h->device);
     free_layers(h);
     if (h->ws) hipFree(h->ws);
+    if (h->gather_ws) hipFree(h->gather_ws);
     for (auto& e : h->pending) {
         hipEventDestroy(e.a);
         hipEventDestroy(e.b);
@@ -437,11 +441,10 @@ static bool expand_gemm_env() {
     return on;
 }
 
-int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream) {
-    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
-    if (!x || !y) return fail(VP3D_ERR_ARG, "x / y is NULL");
-    if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
-    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+// The forward of B windows of T frames.  x: (B, T, J_in*F) f32, or nullptr with `gs`
+// describing where the windows are gathered from (vp3d_forward_windows).
+static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream,
+                        const GatherSrc* gs) {
     int dev = 0;
     hipGetDevice(&dev);
     if (dev != h->device) return fail(VP3D_ERR_STATE, "handle belongs to another device");
@@ -522,7 +525,28 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
         const Act o_type = last ? Act::F32 : act;
         hipError_t e = hipSuccess;
         bool launched = false;
-        if (first && act != Act::F32 && expand_gemm_env() && expand_gemm_eligible(p, o_type, act)) {
+        if (first && gs && act != Act::F32 && expand_gemm_env() && expand_gather_eligible(p, *gs, o_type, act)) {
+            // the window gather (+ camera concat) fused into the expand conv's operand loads
+            e = launch_expand_gemm_gather(p, *gs, act, s);
+            launched = true;
+        } else if (first && gs) {
+            // any other first-layer path: gather the windows into the scratch tensor first
+            const size_t need = (size_t)B * T * L.cin * sizeof(float);
+            if (need > h->gather_bytes) {
+                if (h->gather_ws) HIP_TRY(hipFree(h->gather_ws));
+                h->gather_ws = nullptr;
+                h->gather_bytes = 0;
+                HIP_TRY(hipMalloc(&h->gather_ws, need));
+                h->gather_bytes = need;
+            }
+            hipError_t ge = launch_gather_windows(gs->kps, gs->f2, gs->cams, gs->seq_off, gs->seq_len,
+                                                  gs->pairs, B, T, gs->lead, 0, h->gather_ws, s);
+            if (ge != hipSuccess) return fail(VP3D_ERR_HIP, std::string("gather: ") + hipGetErrorString(ge));
+            x = h->gather_ws;
+            p.A = x;
+        }
+        if (launched) {
+        } else if (first && act != Act::F32 && expand_gemm_env() && expand_gemm_eligible(p, o_type, act)) {
             // 16-bit expand conv straight from the f32 input rows (expand_gemm.hip)
             e = launch_expand_gemm(p, act, s);
             launched = true;
@@ -560,6 +584,36 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
         (void)xin_buf;
     }
     return VP3D_OK;
+}
+
+int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    if (!x || !y) return fail(VP3D_ERR_ARG, "x / y is NULL");
+    if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
+    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    return forward_impl(h, x, B, T, y, dtype, stream, nullptr);
+}
+
+int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const float* cams, const int64_t* seq_off,
+                         const int32_t* seq_len, const int32_t* pairs, int B, int window, int lead, float* y,
+                         int dtype, void* stream) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    if (!kps || !seq_off || !seq_len || !pairs || !y) return fail(VP3D_ERR_ARG, "a device pointer is NULL");
+    if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
+    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    const int cin = h->cfg.num_joints_in * h->cfg.in_features;
+    if (f2 + (cams ? 12 : 0) != cin)
+        return fail(VP3D_ERR_ASSERT, "frame features (" + std::to_string(f2) + (cams ? " + 12" : "") +
+                                         ") != num_joints_in * in_features (" + std::to_string(cin) + ")");
+    GatherSrc g;
+    g.kps = kps;
+    g.f2 = f2;
+    g.cams = cams;
+    g.seq_off = seq_off;
+    g.seq_len = seq_len;
+    g.pairs = pairs;
+    g.lead = lead;
+    return forward_impl(h, nullptr, B, window, y, dtype, stream, &g);
 }
 
 int vp3d_profile_enable(vp3d_handle* h, int enable) {

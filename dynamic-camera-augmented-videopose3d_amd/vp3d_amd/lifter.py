@@ -104,6 +104,40 @@ class NativeLifter:
                     "vp3d_forward")
         return out
 
+    def forward_windows(self, seqs, pairs: torch.Tensor, window: int, lead: int,
+                        concat_cams: bool = False, dtype: str = "fp32",
+                        out: torch.Tensor | None = None) -> torch.Tensor:
+        """Forward of windows gathered on the fly from `seqs` (a pipeline.DeviceSequences):
+        window b = frames [start_b - lead, start_b - lead + window) of sequence seq_b,
+        edge-clamped; with concat_cams the 12 K.E channels follow each frame's keypoints
+        (vp3d_forward_windows: ChunkedGenerator batch + camera concat + TemporalModel forward,
+        the gather fused into the expand conv on the 16-bit path)."""
+        def _idx(d):
+            d = torch.device(d)
+            return (d.type, d.index if d.index is not None else torch.cuda.current_device())
+        if _idx(pairs.device) != _idx(self.device) or _idx(seqs.kps.device) != _idx(self.device):
+            raise RuntimeError("pairs / sequences must live on the model's device")
+        pairs = pairs.contiguous().to(torch.int32)
+        B = int(pairs.shape[0])
+        T_out = self.out_frames(window)
+        if T_out < 1:
+            raise RuntimeError(f"window of {window} frames is invalid for receptive field "
+                               f"{self.receptive_field()}")
+        cams = None
+        if concat_cams:
+            if seqs.cam is None:
+                raise ValueError("no cameras loaded")
+            cams = seqs.cam.data_ptr()
+        if out is None:
+            out = torch.empty((B, T_out, self.num_joints_out, 3), dtype=torch.float32,
+                              device=self.device)
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_forward_windows(
+                self._h, seqs.kps.data_ptr(), seqs.f2, cams, seqs.seq_off.data_ptr(),
+                seqs.seq_len.data_ptr(), pairs.data_ptr(), B, int(window), int(lead), out.data_ptr(),
+                N.DTYPES[dtype], N.stream_ptr(self.device)), "vp3d_forward_windows")
+        return out
+
     # ---- profiling ----
     def profile(self, enable: bool) -> None:
         N.check(self._lib.vp3d_profile_enable(self._h, 1 if enable else 0))

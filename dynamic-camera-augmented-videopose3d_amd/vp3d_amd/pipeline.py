@@ -216,9 +216,18 @@ class SyntheticTrajectoryBatcher:
                                device=self.seqs.device)
         self.k = 0
 
-    def next_batch(self) -> torch.Tensor:
+    def next_pairs(self) -> torch.Tensor:
+        """Per-frame K @ E of every sequence, then the next (B, 2) window table: the
+        inputs of NativeLifter.forward_windows (gather fused into the expand conv)."""
         self.seqs.refresh_cameras()
         p = self.pairs[self.k % self.pairs.shape[0]]
         self.k += 1
-        self.seqs.gather(p, self.window, self.pad, "2d", concat_cams=True, out=self.buf)
+        return p
+
+    def gather(self, pairs: torch.Tensor) -> torch.Tensor:
+        """The (B, window, 23, 2) input tensor of a window table (materialised)."""
+        self.seqs.gather(pairs, self.window, self.pad, "2d", concat_cams=True, out=self.buf)
         return self.buf.view(self.B, self.window, -1, 2)
+
+    def next_batch(self) -> torch.Tensor:
+        return self.gather(self.next_pairs())

@@ -111,6 +111,23 @@ int vp3d_reserve(vp3d_handle* h, int B, int T, int dtype);
  * Launches on `stream`; returns without synchronising. */
 int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream);
 
+/* Eval-mode forward of B windows gathered on the fly from device-resident
+ * sequences: the ChunkedGenerator batch (generators.py:102-137; edge padding of
+ * pad_chunk :92-100) and the trajectory concat (CamTransformer.py:187-190) feeding
+ * TemporalModelBase.forward (TemporalModel.py:62-76) without materialising the
+ * (B, window, J_in*F) input.  On the 16-bit path the gather is fused into the
+ * expand conv's operand loads; otherwise the windows go through a scratch tensor.
+ *   kps:     device f32 (n_frames, f2) normalised keypoints of all sequences
+ *   cams:    device f32 (n_frames, 12) per-frame K.E, or NULL (no concat);
+ *            f2 (+ 12) must equal num_joints_in * in_features
+ *   seq_off: device int64 first frame of each sequence; seq_len: device int32
+ *   pairs:   device int32 (B, 2) = (sequence, start); window b = sequence frames
+ *            [start - lead, start - lead + window), clamped to [0, len-1]
+ *   y:       device f32 (B, vp3d_out_frames(window), J_out, 3) */
+int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const float* cams,
+                         const int64_t* seq_off, const int32_t* seq_len, const int32_t* pairs, int B,
+                         int window, int lead, float* y, int dtype, void* stream);
+
 /* ---- per-layer timing (HIP events recorded on the launch stream) ---- */
 int vp3d_profile_enable(vp3d_handle* h, int enable);
 /* Number of kernel launches one forward makes (conv layers incl. shrink). */

@@ -126,3 +126,49 @@ def test_gather_edge_cases():
     assert np.array_equal(out[3], s0[np.clip(np.arange(-1, 6), 0, 4)])
     empty = ds.gather(pairs[:0], 7, 3, "2d")
     assert empty.shape == (0, 7, 4)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("traj", [True, False])
+def test_forward_windows_matches_gather_then_forward(dtype, traj):
+    """vp3d_forward_windows (window gather + camera concat fused into the expand conv's
+    operand loads on the 16-bit path, a scratch gather on fp32) gives exactly the output
+    of gathering the windows first and running the forward on them; windows overhang both
+    ends of their sequences (edge clamping) and one sequence is shorter than a window."""
+    from helpers import make_model
+    from vp3d_amd.pipeline import DeviceSequences
+    jin = 23 if traj else 17
+    model, _ = make_model(True, jin=jin, channels=256)
+    model.cuda()
+    lens = [300, 40, 1000, 243]
+    kps, cams = [], []
+    for i, n in enumerate(lens):
+        kps.append(synth.normalized_windows(11 + i, f"fw{i}", 1, n)[0])
+        cams.append({"intrinsics": synth.CMU_INTRINSICS,
+                     "extrinsics": synth.camera_extrinsics(5, f"fw{i}", n)})
+    ds = DeviceSequences(kps, None, cams if traj else None, "cuda")
+    rng = np.random.RandomState(3)
+    B = 777
+    seq = rng.randint(0, len(lens), size=B)
+    start = np.array([rng.randint(-150, lens[s] + 150) for s in seq])
+    pairs = torch.from_numpy(np.stack([seq, start], -1).astype(np.int32)).cuda()
+    lead = 121
+    lifter = model.native_lifter(torch.device("cuda", torch.cuda.current_device()))
+    with torch.no_grad():
+        y = lifter.forward_windows(ds, pairs, 243, lead, concat_cams=traj, dtype=dtype)
+        x = ds.gather(pairs, 243, lead, "2d", concat_cams=traj).view(B, 243, jin, 2)
+        y_ref = lifter.forward(x, dtype)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref), (y - y_ref).abs().max().item()
+
+
+def test_forward_windows_rejects_feature_mismatch():
+    from helpers import make_model
+    from vp3d_amd.pipeline import DeviceSequences
+    model, _ = make_model(True, jin=23, channels=64, fw=(3, 3))
+    model.cuda()
+    ds = DeviceSequences([synth.normalized_windows(1, "rej", 1, 50)[0]], None, None, "cuda")
+    pairs = torch.zeros((2, 2), dtype=torch.int32, device="cuda")
+    lifter = model.native_lifter(torch.device("cuda", torch.cuda.current_device()))
+    with pytest.raises(AssertionError):
+        lifter.forward_windows(ds, pairs, 9, 4, concat_cams=False)
