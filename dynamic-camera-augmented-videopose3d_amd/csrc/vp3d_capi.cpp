@@ -949,4 +949,14 @@ int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_poin
     return VP3D_OK;
 }
 
+
+int vp3d_pose_metrics(const float* pred, const float* target, int64_t n_frames, int32_t n_joints, double* acc,
+                      void* stream) {
+    if (n_frames < 0 || n_joints <= 0) return fail(VP3D_ERR_ASSERT, "shape mismatch");
+    if (!acc || (n_frames > 0 && (!pred || !target))) return fail(VP3D_ERR_ARG, "pred / target / acc is NULL");
+    hipError_t e = launch_pose_metrics(pred, target, n_frames, n_joints, acc, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(VP3D_ERR_HIP, std::string("pose_metrics: ") + hipGetErrorString(e));
+    return VP3D_OK;
+}
+
 }  // extern "C"

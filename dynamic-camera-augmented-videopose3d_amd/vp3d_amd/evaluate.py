@@ -21,8 +21,10 @@ import torch
 
 
 class DeviceMetrics:
-    """Protocol #1 through the libvp3d reduction kernel; the post-path protocols
-     with torch ops on the same device."""
+    """All four protocols through libvp3d kernels on the predictions' device: Protocol
+    #1 the mpjpe reduction, P-MPJPE / N-MPJPE / MPJVE the vp3d_pose_metrics kernel
+    (csrc/metrics.hip).  P-MPJPE and MPJVE are returned as
+    numpy float32 scalars like the reference's numpy implementations."""
 
     def __init__(self):
         from . import pipeline
@@ -32,31 +34,16 @@ class DeviceMetrics:
         return float(self._p.mpjpe(pred, gt))
 
     def n_mpjpe(self, pred: torch.Tensor, gt: torch.Tensor) -> float:
-        pp = torch.mean(torch.sum(pred ** 2, dim=3, keepdim=True), dim=2, keepdim=True)
-        pt = torch.mean(torch.sum(gt * pred, dim=3, keepdim=True), dim=2, keepdim=True)
-        return self.mpjpe((pt / pp) * pred, gt)
+        acc = self._p.pose_metrics(pred, gt)
+        return float((acc[2] / acc[4]).float())
 
-    def p_mpjpe(self, pred: torch.Tensor, gt: torch.Tensor) -> float:
-        X, Y = gt.double(), pred.double()
-        mx, my = X.mean(dim=1, keepdim=True), Y.mean(dim=1, keepdim=True)
-        x0, y0 = X - mx, Y - my
-        nx = torch.sqrt((x0 ** 2).sum(dim=(1, 2), keepdim=True))
-        ny = torch.sqrt((y0 ** 2).sum(dim=(1, 2), keepdim=True))
-        x0, y0 = x0 / nx, y0 / ny
-        U, s, Vt = torch.linalg.svd(x0.transpose(1, 2) @ y0)
-        V = Vt.transpose(1, 2)
-        R = V @ U.transpose(1, 2)
-        sgn = torch.sign(torch.linalg.det(R)).unsqueeze(1)
-        V[:, :, -1] *= sgn
-        s[:, -1] *= sgn.flatten()
-        R = V @ U.transpose(1, 2)
-        a = s.sum(dim=1, keepdim=True).unsqueeze(2) * nx / ny
-        t = mx - a * (my @ R)
-        aligned = a * (Y @ R) + t
-        return float(torch.linalg.norm(aligned - X, dim=-1).mean())
+    def p_mpjpe(self, pred: torch.Tensor, gt: torch.Tensor):
+        acc = self._p.pose_metrics(pred, gt).cpu().numpy()
+        return np.float32(acc[1] / acc[4])
 
-    def mpjve(self, pred: torch.Tensor, gt: torch.Tensor) -> float:
-        return float(torch.linalg.norm(torch.diff(pred, dim=0) - torch.diff(gt, dim=0), dim=-1).mean())
+    def mpjve(self, pred: torch.Tensor, gt: torch.Tensor):
+        acc = self._p.pose_metrics(pred, gt).cpu().numpy()
+        return np.float32(acc[3] / acc[5])
 
 
 def evaluate(generator, model: Callable, metrics, action: str | None = None, verbose: bool = True):

@@ -110,6 +110,25 @@ def mpjpe_sums(pred: torch.Tensor, target: torch.Tensor, acc: Optional[torch.Ten
     return acc
 
 
+def pose_metrics(pred: torch.Tensor, target: torch.Tensor, acc: Optional[torch.Tensor] = None
+                 ) -> torch.Tensor:
+    """vp3d_pose_metrics over (..., J, 3) poses whose leading axes flatten to frames in
+    time order: accumulates (float64, device) [MPJPE, P-MPJPE, N-MPJPE, MPJVE error sums,
+    n_frames*J, (n_frames-1)*J]."""
+    _require_cuda(pred, "pred")
+    _require_cuda(target, "target")
+    assert pred.shape == target.shape and pred.shape[-1] == 3
+    J = int(pred.shape[-2])
+    pred = pred.contiguous().float()
+    target = target.contiguous().float()
+    if acc is None:
+        acc = torch.zeros(6, dtype=torch.float64, device=pred.device)
+    with torch.cuda.device(pred.device):
+        N.check(N.load().vp3d_pose_metrics(pred.data_ptr(), target.data_ptr(), pred.numel() // (3 * J), J,
+                                           acc.data_ptr(), _stream(pred)), "vp3d_pose_metrics")
+    return acc
+
+
 def mpjpe(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     """Mean per-joint position error (device scalar, float32 like torch.mean)."""
     acc = mpjpe_sums(pred, target)

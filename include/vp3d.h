@@ -212,6 +212,16 @@ int vp3d_gather_windows(const float* kps, int32_t f2, const float* cams, const i
 int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_points, double* acc,
                           void* stream);
 
+/* Evaluation metrics of one sequence's predictions (run.py:732-750): partial sums of
+ * MPJPE (loss.py:11-17), P-MPJPE (rigid alignment per frame, loss.py:29-68), N-MPJPE
+ * (per-frame scale, loss.py:70-80) and MPJVE (first difference along frames,
+ * loss.py:82-91) over pred / target (n_frames, n_joints, 3), float64:
+ *   acc[0..3] += summed per-joint errors (MPJPE, P-MPJPE, N-MPJPE, MPJVE)
+ *   acc[4] += n_frames * n_joints,  acc[5] += (n_frames - 1) * n_joints
+ * acc: device f64[6] (caller zeroes).  Metric = acc[i] / acc[4] (i < 3), acc[3] / acc[5]. */
+int vp3d_pose_metrics(const float* pred, const float* target, int64_t n_frames, int32_t n_joints,
+                      double* acc, void* stream);
+
 const char* vp3d_last_error(void);
 int vp3d_abi_version(void);
 
