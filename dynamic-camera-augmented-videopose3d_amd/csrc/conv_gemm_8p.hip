@@ -53,7 +53,8 @@ __device__ __forceinline__ void vmw() {
 }
 
 // ABL (ablation, measurement only): 0 = normal, 1 = no LDS-DMA inside the K loop
-// (MFMA + LDS reads on stale data), 2 = no MFMAs (memory traffic only).
+// (MFMA + LDS reads on stale data), 2 = no MFMAs (memory traffic only), 3 = no
+// fragment reads after the first K-step (DMA + MFMA), 4 = neither reads nor DMA.
 template <typename CT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[PRING + 2 * PMAXN * 4];
@@ -146,11 +147,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     for (int s = 0; s < nk; ++s) {
         const char* slot = smem + (s % PSLOTS) * PSLOT_BYTES;
         // ---- segment A: B fragments + A rows 0-63 of stage s; A pieces of stage s+2
+        if (ABL < 3 || s == 0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bf[j] = *(const u32x4*)(slot + b_frag_off + j * 16 * 64);
+            for (int j = 0; j < 4; ++j) bf[j] = *(const u32x4*)(slot + b_frag_off + j * 16 * 64);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) alo[i] = *(const u32x4*)(slot + a_frag_off + i * 16 * 64);
-        if (ABL != 1 && s + 2 < nk) issue_a(s + 2);
+            for (int i = 0; i < 4; ++i) alo[i] = *(const u32x4*)(slot + a_frag_off + i * 16 * 64);
+        }
+        if (ABL != 1 && ABL != 4 && s + 2 < nk) issue_a(s + 2);
         // the residual block of this wave, two K-steps before the end: the tail's
         // vmcnt(0) in segment B retires it, the epilogue never waits for it
         if (p.R && s == (nk >= 2 ? nk - 2 : 0)) load_residual_tp<CT, 8>(p, res, m0 + wr * 128, n0 + wc * 64, lane);
@@ -167,10 +170,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
         __builtin_amdgcn_s_setprio(0);
         barrier_pinned();
         // ---- segment B: A rows 64-127 of stage s; B pieces of stage s+3; wait stage s+1
+        if (ABL < 3 || s == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ahi[i] = *(const u32x4*)(slot + a_frag_off + (4 + i) * 16 * 64);
+            for (int i = 0; i < 4; ++i) ahi[i] = *(const u32x4*)(slot + a_frag_off + (4 + i) * 16 * 64);
+        }
         if (s + 3 < nk) {
-            if (ABL != 1) issue_b(s + 3);
+            if (ABL != 1 && ABL != 4) issue_b(s + 3);
             vmw<6>();  // younger than stage s+1: B(s+2), A(s+2), B(s+3)
         } else if (s + 2 < nk) {
             vmw<4>();  // B(s+2), A(s+2)
@@ -219,6 +224,10 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 1>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16 && abl == 2)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 2>), grid, dim3(512), 0, stream, p);
+    else if (compute == Act::BF16 && abl == 3)
+        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 3>), grid, dim3(512), 0, stream, p);
+    else if (compute == Act::BF16 && abl == 4)
+        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 4>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16>), grid, dim3(512), 0, stream, p);
     else
