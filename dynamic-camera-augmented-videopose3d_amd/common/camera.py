@@ -6,8 +6,9 @@ HIP tensors stay on device; numpy arrays (the reference's calling convention at
 dataset-load time, run.py:78,117,123) are moved to the current device, computed
 there and returned as float32 numpy — exactly the values run.py stores (the
 reference computes the offset in float64 and writes the result back into its
-float32 arrays, quirk Q6).  The H36M distortion projections (:37-90) are
-offline-prep only and out of scope.
+float32 arrays, quirk Q6).  The H36M projections project_to_2d (:37-67, radial +
+tangential distortion) and project_to_2d_linear (:69-90) are one libvp3d kernel
+(vp3d_project_to_2d) over HIP tensors (the H36M camera path).
 """
 import numpy as np
 import torch
@@ -49,3 +50,19 @@ def camera_to_world(X, R, t):
     out = _P.world_to_camera(Xd, Rinv, np.zeros(3, np.float32)) + torch.as_tensor(
         np.asarray(t, dtype=np.float32), device=Xd.device)
     return out.cpu().numpy() if host else out
+
+
+def project_to_2d(X, camera_params):
+    assert X.shape[-1] == 3
+    assert len(camera_params.shape) == 2
+    assert camera_params.shape[-1] == 9
+    assert X.shape[0] == camera_params.shape[0]
+    return _P.project_to_2d(X, torch.as_tensor(camera_params, device=X.device), linear=False)
+
+
+def project_to_2d_linear(X, camera_params):
+    assert X.shape[-1] == 3
+    assert len(camera_params.shape) == 2
+    assert camera_params.shape[-1] == 9
+    assert X.shape[0] == camera_params.shape[0]
+    return _P.project_to_2d(X, torch.as_tensor(camera_params, device=X.device), linear=True)

@@ -7,6 +7,7 @@
 //                      :193-198, fused with the trajectory concat of
 //                      common/models/CamTransformer.py:187-190
 //   mpjpe_accumulate   reference common/loss.py:11-17
+//   project_to_2d      reference common/camera.py:37-67 (H36M distortion), :69-90 (linear)
 //
 // Floating-point contraction is OFF (build flag -ffp-contract=off, plus the pragma
 // below): HIP compiles with -ffp-contract=fast by default and __fadd_rn/__fmul_rn
@@ -154,7 +155,45 @@ __global__ void mpjpe_kernel(const float* __restrict__ pred, const float* __rest
     }
 }
 
+// H36M camera projection of camera-space points, one thread per point; camera of
+// point i = i / pts_per_cam, params [f(2), c(2), k(3), p(2)].  The torch-float32
+// op order of camera.py:59-67: XX = clamp(X_xy / X_z, -1, 1); r2 = (0 + x^2) + y^2;
+// radial = 1 + (((0 + k1 r2) + k2 r2^2) + k3 r2^3) with r2^3 = (r2 r2) r2 (ATen's pow
+// for exponent 3); tan = (0 + p1 x) + p2 y; out = f * (XX (radial + tan) + p r2) + c.
+__global__ void project_to_2d_kernel(const float* __restrict__ X, int64_t n, int64_t pts_per_cam,
+                                     const float* __restrict__ prm, int linear, float* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float* q = prm + (i / pts_per_cam) * 9;
+        const float z = X[3 * i + 2];
+        float u = X[3 * i] / z, v = X[3 * i + 1] / z;
+        u = fminf(fmaxf(u, -1.f), 1.f);
+        v = fminf(fmaxf(v, -1.f), 1.f);
+        float ox = u, oy = v;
+        if (!linear) {
+            const float r2 = u * u + v * v;
+            const float r4 = r2 * r2;
+            const float r6 = r4 * r2;
+            const float radial = 1.f + ((q[4] * r2 + q[5] * r4) + q[6] * r6);
+            const float tan = q[7] * u + q[8] * v;
+            ox = u * (radial + tan) + q[7] * r2;
+            oy = v * (radial + tan) + q[8] * r2;
+        }
+        out[2 * i] = q[0] * ox + q[2];
+        out[2 * i + 1] = q[1] * oy + q[3];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_cam, const float* params,
+                                bool linear, float* out, hipStream_t s) {
+    const int64_t n = n_cams * pts_per_cam;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(project_to_2d_kernel, grid_for(n, 4), dim3(kThreads), 0, s, X, n, pts_per_cam, params,
+                       linear ? 1 : 0, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, float* out,
                                    bool inverse, hipStream_t s) {

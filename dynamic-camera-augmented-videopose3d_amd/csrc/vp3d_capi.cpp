@@ -950,6 +950,14 @@ int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_poin
 }
 
 
+int vp3d_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_cam, const float* params, int32_t linear,
+                       float* out, void* stream) {
+    if (n_cams < 0 || pts_per_cam < 0) return fail(VP3D_ERR_ASSERT, "shape mismatch");
+    if (n_cams * pts_per_cam > 0 && (!X || !params || !out)) return fail(VP3D_ERR_ARG, "bad pointer");
+    HIP_TRY(launch_project_to_2d(X, n_cams, pts_per_cam, params, linear != 0, out, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
 int vp3d_pose_metrics(const float* pred, const float* target, int64_t n_frames, int32_t n_joints, double* acc,
                       void* stream) {
     if (n_frames < 0 || n_joints <= 0) return fail(VP3D_ERR_ASSERT, "shape mismatch");

@@ -44,7 +44,7 @@ EXPORTS = [
     "vp3d_reserve", "vp3d_forward", "vp3d_forward_windows", "vp3d_profile_enable", "vp3d_layer_count",
     "vp3d_profile_read", "vp3d_profile_reset", "vp3d_normalize_screen",
     "vp3d_image_coordinates", "vp3d_camera_matrices", "vp3d_world_to_camera",
-    "vp3d_gather_windows", "vp3d_mpjpe_accumulate", "vp3d_pose_metrics", "vp3d_last_error", "vp3d_abi_version",
+    "vp3d_gather_windows", "vp3d_mpjpe_accumulate", "vp3d_pose_metrics", "vp3d_project_to_2d", "vp3d_last_error", "vp3d_abi_version",
     "vp3d_stream_create", "vp3d_stream_reset", "vp3d_stream_io", "vp3d_stream_step",
     "vp3d_stream_frames_seen", "vp3d_stream_graph_capture", "vp3d_stream_graph_launch",
     "vp3d_stream_destroy",
@@ -96,6 +96,7 @@ _SIGNATURES = {
     "vp3d_gather_windows": (_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
     "vp3d_mpjpe_accumulate": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "vp3d_pose_metrics": (_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "vp3d_project_to_2d": (_int, [_vp, _i64, _i64, _vp, _i32, _vp, _vp]),
     "vp3d_stream_create": (_int, [_vp, _int, ctypes.POINTER(_vp)]),
     "vp3d_stream_reset": (_int, [_vp, _vp]),
     "vp3d_stream_io": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_int)]),

@@ -110,6 +110,23 @@ def mpjpe_sums(pred: torch.Tensor, target: torch.Tensor, acc: Optional[torch.Ten
     return acc
 
 
+def project_to_2d(X: torch.Tensor, camera_params: torch.Tensor, linear: bool = False) -> torch.Tensor:
+    """H36M projection (vp3d_project_to_2d) of camera-space points X (N, *, 3) with
+    per-row intrinsics camera_params (N, 9) -> (N, *, 2)."""
+    _require_cuda(X, "X")
+    assert X.shape[-1] == 3 and camera_params.dim() == 2 and camera_params.shape[-1] == 9
+    assert X.shape[0] == camera_params.shape[0]
+    Xc = X.contiguous().float()
+    prm = camera_params.to(Xc.device).contiguous().float()
+    n = int(X.shape[0])
+    per = Xc.numel() // (3 * n) if n else 0
+    out = torch.empty((*X.shape[:-1], 2), dtype=torch.float32, device=Xc.device)
+    with torch.cuda.device(Xc.device):
+        N.check(N.load().vp3d_project_to_2d(Xc.data_ptr(), n, per, prm.data_ptr(), 1 if linear else 0,
+                                            out.data_ptr(), _stream(Xc)), "vp3d_project_to_2d")
+    return out
+
+
 def pose_metrics(pred: torch.Tensor, target: torch.Tensor, acc: Optional[torch.Tensor] = None
                  ) -> torch.Tensor:
     """vp3d_pose_metrics over (..., J, 3) poses whose leading axes flatten to frames in

@@ -207,6 +207,14 @@ int vp3d_gather_windows(const float* kps, int32_t f2, const float* cams, const i
                         const int32_t* seq_len, const int32_t* pairs, int32_t B, int32_t window,
                         int32_t pad, int32_t causal_shift, float* out, void* stream);
 
+/* project_to_2d (camera.py:37-67: H36M radial + tangential distortion) or, with
+ * linear != 0, project_to_2d_linear (:69-90): X device f32 (n_cams, pts_per_cam, 3)
+ * camera-space points, params device f32 (n_cams, 9) = [f(2), c(2), k(3), p(2)],
+ * out device f32 (n_cams, pts_per_cam, 2).  Same float32 operation order as the
+ * reference's torch code (bit-exact on the goldens). */
+int vp3d_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_cam, const float* params,
+                       int32_t linear, float* out, void* stream);
+
 /* mpjpe partial sums (loss.py:11-17): acc[0] += sum ||pred - target||_2 over
  * n_points xyz triples, acc[1] += n_points.  acc: device f64[2] (caller zeroes). */
 int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_points, double* acc,

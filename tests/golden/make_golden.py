@@ -20,7 +20,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 PKG = os.path.join(REPO, "dynamic-camera-augmented-videopose3d_amd")
-REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+REF = os.environ.get("VP3D_REFERENCE", "/root/reference")
 
 # `common` must resolve to the reference (a namespace package there, so our
 # regular package must not be on sys.path); vp3d_amd.synth is loaded by file path.
@@ -163,6 +163,26 @@ def camera_goldens():
     save("camera", **a)
 
 
+def projection_goldens():
+    """H36M projections (camera.py:37-67 with distortion, :69-90 linear): camera-space
+    points (positive depth, some beyond the [-1, 1] clamp of X/Z) and H36M-style
+    intrinsics [f(2), c(2), k(3), p(2)] per camera."""
+    a = {}
+    n_cam, n_pts = 6, 2 * 17
+    X = synth.normal(6, "proj/X", (n_cam, n_pts, 3), 1.0).astype(np.float32)
+    X[..., 2] = np.abs(X[..., 2]) * 2 + 0.2
+    X[0, :4, 2] = 0.3  # |X/Z| > 1: exercises the clamp
+    prm = np.concatenate([
+        1.1 + 0.1 * synth.normal(6, "proj/f", (n_cam, 2), 1.0),
+        0.05 * synth.normal(6, "proj/c", (n_cam, 2), 1.0),
+        0.1 * synth.normal(6, "proj/k", (n_cam, 3), 1.0),
+        0.01 * synth.normal(6, "proj/p", (n_cam, 2), 1.0)], axis=1).astype(np.float32)
+    a["X"], a["params"] = X, prm
+    a["proj"] = ref_camera.project_to_2d(torch.from_numpy(X), torch.from_numpy(prm)).numpy()
+    a["proj_linear"] = ref_camera.project_to_2d_linear(torch.from_numpy(X), torch.from_numpy(prm)).numpy()
+    save("projection", **a)
+
+
 def loss_goldens():
     a = {}
     pred = synth.normal(5, "pred", (2, 40, 17, 3), 0.2).astype(np.float32)
@@ -226,14 +246,23 @@ def run_eval_golden():
                                                            subjects=3, actions=3, frames=200))))
 
 
+GROUPS = {"run_eval": run_eval_golden, "model": model_goldens, "generator": generator_goldens,
+          "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens}
+
 if __name__ == "__main__":
-    run_eval_golden()
-    model_goldens()
-    generator_goldens()
-    camera_goldens()
-    loss_goldens()
+    # python make_golden.py [group ...]  (default: every group); the manifest is merged
+    todo = sys.argv[1:] or list(GROUPS)
+    for g in todo:
+        GROUPS[g]()
     env = dict(torch=torch.__version__, numpy=np.__version__, python=sys.version.split()[0],
                reference=REF)
-    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+    mpath = os.path.join(HERE, "MANIFEST.json")
+    fixtures = {}
+    if os.path.exists(mpath) and sys.argv[1:]:
+        with open(mpath) as f:
+            fixtures = json.load(f).get("fixtures", {})
+    fixtures.update(MANIFEST)
+    MANIFEST = fixtures
+    with open(mpath, "w") as f:
         json.dump({"environment": env, "fixtures": MANIFEST}, f, indent=1, sort_keys=True)
     print("total KiB", sum(v["bytes"] for v in MANIFEST.values()) / 1024)

@@ -172,3 +172,16 @@ def test_forward_windows_rejects_feature_mismatch():
     lifter = model.native_lifter(torch.device("cuda", torch.cuda.current_device()))
     with pytest.raises(AssertionError):
         lifter.forward_windows(ds, pairs, 9, 4, concat_cams=False)
+
+
+@pytest.mark.parametrize("linear", [False, True])
+def test_project_to_2d_bit_exact(linear):
+    """H36M projection (camera.py:37-67 / :69-90) bit-exact vs the reference's own
+    outputs (tests/golden/projection.npz), including points beyond the X/Z clamp."""
+    from common.camera import project_to_2d, project_to_2d_linear
+    g = load("projection")
+    X = torch.from_numpy(g["X"]).cuda()
+    P = torch.from_numpy(g["params"]).cuda()
+    out = (project_to_2d_linear if linear else project_to_2d)(X, P)
+    assert out.shape == tuple(g["proj"].shape)
+    assert np.array_equal(out.cpu().numpy(), g["proj_linear" if linear else "proj"])

@@ -154,6 +154,12 @@ def test_oracle_world_to_camera():
     np.testing.assert_allclose(back, g["c2w_out"], atol=0)
 
 
+def test_oracle_projection():
+    g = load("projection")
+    assert np.array_equal(camera_ref.project_to_2d(g["X"], g["params"]).numpy(), g["proj"])
+    assert np.array_equal(camera_ref.project_to_2d_linear(g["X"], g["params"]).numpy(), g["proj_linear"])
+
+
 def test_oracle_losses():
     g = load("loss")
     p, t = torch.from_numpy(g["pred"]), torch.from_numpy(g["tgt"])
