@@ -1,0 +1,93 @@
+// Host-side state shared by the C-ABI translation units (vp3d_capi.cpp: eval
+// forward + streaming; vp3d_train.cpp: the training step).  Not part of the
+// public boundary (include/vp3d.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vp3d.h"
+
+namespace vp3d {
+namespace host {
+
+// Record `msg` as the calling thread's last error (vp3d_last_error) and return `code`.
+int fail(int code, const std::string& msg);
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return ::vp3d::host::fail(_e == hipErrorOutOfMemory ? VP3D_ERR_OOM : VP3D_ERR_HIP, \
+                                      std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+inline uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+inline uint16_t f32_to_f16_rne(float f) {
+    _Float16 h = (_Float16)f;
+    uint16_t r;
+    std::memcpy(&r, &h, 2);
+    return r;
+}
+
+// One convolution of the stack (expand, k-conv / 1x1 of each block, shrink).
+struct Layer {
+    int cin = 0, cout = 0, taps = 1, dil = 1, stride = 1;  // conv geometry
+    int K = 0, Kp = 0, Np = 0, Ktap = 0, gemm_taps = 1;     // GEMM geometry
+    bool relu = true;
+    bool residual = false;  // 1x1 conv of a block: add the block-input slice
+    int res_stride = 1, res_off = 0;
+    float* w32 = nullptr;
+    uint16_t* wbf = nullptr;
+    uint16_t* wh = nullptr;
+    float* scale = nullptr;
+    float* shift = nullptr;
+};
+
+struct ProfEvent {
+    int layer;
+    hipEvent_t a, b;
+    double flop;
+};
+
+// Shape rules of TemporalModel.py (validation :20-21, geometry :31,85-124,152-186).
+int validate_cfg(const vp3d_cfg* c);
+// pad / causal_shift and the per-layer conv + GEMM geometry.
+void build_geometry(const vp3d_cfg& c, std::vector<int>& pad, std::vector<int>& causal_shift,
+                    std::vector<Layer>& layers);
+// Temporal length after each layer for T input frames; false if T does not fit.
+bool layer_lengths(const vp3d_cfg& c, const std::vector<int>& pad, const std::vector<Layer>& layers, int T,
+                   std::vector<int>& len);
+
+}  // namespace host
+}  // namespace vp3d
+
+struct vp3d_handle {
+    vp3d_cfg cfg{};
+    int device = 0;
+    std::vector<int> pad, causal_shift;
+    std::vector<vp3d::host::Layer> layers;  // expand, (conv_k, conv_1x1) per block, shrink
+    // activation workspace: three rotating buffers
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    // window-gather scratch of vp3d_forward_windows when the fused expand path does not apply
+    float* gather_ws = nullptr;
+    size_t gather_bytes = 0;
+    // profiling
+    bool profiling = false;
+    std::vector<vp3d::host::ProfEvent> pending;
+    std::vector<hipEvent_t> free_events;
+    std::vector<double> prof_ms;
+    std::vector<int64_t> prof_n;
+    std::vector<double> prof_flop;
+};

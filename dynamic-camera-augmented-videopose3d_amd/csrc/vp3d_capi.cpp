@@ -21,10 +21,12 @@
 
 #include "../../include/vp3d.h"
 #include "kernels.h"
+#include "host.h"
 
 using namespace vp3d;
 
-namespace {
+namespace vp3d {
+namespace host {
 
 thread_local std::string g_last_error;
 
@@ -33,71 +35,13 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                   \
-    do {                                                                                \
-        hipError_t _e = (expr);                                                         \
-        if (_e != hipSuccess)                                                           \
-            return fail(_e == hipErrorOutOfMemory ? VP3D_ERR_OOM : VP3D_ERR_HIP,         \
-                        std::string(#expr) + ": " + hipGetErrorString(_e));             \
-    } while (0)
+}  // namespace host
+}  // namespace vp3d
 
-uint16_t f32_to_bf16_rne(float f) {
-    uint32_t u;
-    std::memcpy(&u, &f, 4);
-    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
-}
+using namespace vp3d::host;
 
-uint16_t f32_to_f16_rne(float f) {
-    _Float16 h = (_Float16)f;
-    uint16_t r;
-    std::memcpy(&r, &h, 2);
-    return r;
-}
-
-struct Layer {
-    int cin = 0, cout = 0, taps = 1, dil = 1, stride = 1;  // conv geometry
-    int K = 0, Kp = 0, Np = 0, Ktap = 0, gemm_taps = 1;     // GEMM geometry
-    bool relu = true;
-    bool residual = false;  // 1x1 conv of a block: add the block-input slice
-    int res_stride = 1, res_off = 0;
-    float* w32 = nullptr;
-    uint16_t* wbf = nullptr;
-    uint16_t* wh = nullptr;
-    float* scale = nullptr;
-    float* shift = nullptr;
-};
-
-struct ProfEvent {
-    int layer;
-    hipEvent_t a, b;
-    double flop;
-};
-
-}  // namespace
-
-struct vp3d_handle {
-    vp3d_cfg cfg{};
-    int device = 0;
-    std::vector<int> pad, causal_shift;
-    std::vector<Layer> layers;  // expand, (conv_k, conv_1x1) per block, shrink
-    // activation workspace: three buffers of ws_elems elements of ws_esize bytes
-    void* ws = nullptr;
-    size_t ws_bytes = 0;
-    // window-gather scratch of vp3d_forward_windows when the fused expand path does not apply
-    float* gather_ws = nullptr;
-    size_t gather_bytes = 0;
-    // profiling
-    bool profiling = false;
-    std::vector<ProfEvent> pending;
-    std::vector<hipEvent_t> free_events;
-    std::vector<double> prof_ms;
-    std::vector<int64_t> prof_n;
-    std::vector<double> prof_flop;
-};
-
-namespace {
+namespace vp3d {
+namespace host {
 
 int validate_cfg(const vp3d_cfg* c) {
     if (!c) return fail(VP3D_ERR_ARG, "cfg is NULL");
@@ -118,8 +62,13 @@ int validate_cfg(const vp3d_cfg* c) {
 }
 
 // pad / causal_shift bookkeeping (TemporalModel.py:31,107-111 and :173-177)
-void build_geometry(vp3d_handle* h) {
-    const vp3d_cfg& c = h->cfg;
+void build_geometry(const vp3d_cfg& c, std::vector<int>& pad_out, std::vector<int>& shift_out,
+                    std::vector<Layer>& layers_out) {
+    struct {
+        std::vector<int>& pad;
+        std::vector<int>& causal_shift;
+        std::vector<Layer>& layers;
+    } hh{pad_out, shift_out, layers_out}, *h = &hh;
     const int* fw = c.filter_widths;
     const bool f1 = c.variant == VP3D_VARIANT_STRIDED_1F;
     h->pad.assign(1, fw[0] / 2);
@@ -200,6 +149,13 @@ void build_geometry(vp3d_handle* h) {
     }
 }
 
+}  // namespace host
+}  // namespace vp3d
+
+namespace {
+
+void build_geometry(vp3d_handle* h) { build_geometry(h->cfg, h->pad, h->causal_shift, h->layers); }
+
 void free_layers(vp3d_handle* h) {
     for (Layer& L : h->layers) {
         hipFree(L.w32);
@@ -276,7 +232,18 @@ int upload_weights(vp3d_handle* h, const float* const* w, int n) {
 // Temporal length after each layer for an input of T frames; returns false if
 // T is too short or the residual slice would not line up with the block output
 // (the reference raises in that case: a size-mismatched add).
-bool layer_lengths(const vp3d_handle* h, int T, std::vector<int>& len) {
+}  // namespace
+
+namespace vp3d {
+namespace host {
+
+bool layer_lengths(const vp3d_cfg& cfg, const std::vector<int>& pad, const std::vector<Layer>& layers, int T,
+                   std::vector<int>& len) {
+    struct {
+        const vp3d_cfg& cfg;
+        const std::vector<int>& pad;
+        const std::vector<Layer>& layers;
+    } hh{cfg, pad, layers}, *h = &hh;
     len.clear();
     int L = T;
     for (const Layer& ly : h->layers) {
@@ -303,6 +270,15 @@ bool layer_lengths(const vp3d_handle* h, int T, std::vector<int>& len) {
         if (rlen != lout) return false;
     }
     return true;
+}
+
+}  // namespace host
+}  // namespace vp3d
+
+namespace {
+
+bool layer_lengths(const vp3d_handle* h, int T, std::vector<int>& len) {
+    return layer_lengths(h->cfg, h->pad, h->layers, T, len);
 }
 
 size_t esize(int dtype) { return dtype == VP3D_DTYPE_F32 ? 4 : 2; }

@@ -20,7 +20,8 @@ BUILD_DIR = os.path.join(ROOT_PKG, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libvp3d.so")
 
 SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_persist.hip", "conv_gemm_pp.hip", "expand_gemm.hip", "conv_gemm_tp.hip", "conv_gemm_8p.hip", "preprocess.hip", "metrics.hip", "stream_step.hip", "vp3d_capi.cpp"]
-HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "gemm_common.h"), os.path.join(INCLUDE, "vp3d.h")]
+HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "gemm_common.h"), os.path.join(CSRC, "host.h"),
+           os.path.join(INCLUDE, "vp3d.h")]
 ARCH = os.environ.get("VP3D_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -46,9 +47,13 @@ def _run(cmd):
     return r.stdout
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> str:
+    """Compile every stale translation unit (in parallel: hipcc is single-threaded
+    per file) and link libvp3d.so."""
+    from concurrent.futures import ThreadPoolExecutor
+
     os.makedirs(BUILD_DIR, exist_ok=True)
-    objs = []
+    objs, todo = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         if not os.path.exists(src):
@@ -60,11 +65,16 @@ def build(verbose: bool = False, force: bool = False) -> str:
                 cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON_FLAGS + ["-c", src, "-o", obj]
             else:
                 cmd = [HIPCC] + COMMON_FLAGS + ["-c", src, "-o", obj]
+            todo.append(cmd)
+    if todo:
+        jobs = jobs or max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+        for cmd in todo:
             if verbose:
                 print("$", " ".join(cmd), flush=True)
-            out = _run(cmd)
-            if verbose and out.strip():
-                print(out)
+        with ThreadPoolExecutor(jobs) as ex:
+            for out in ex.map(_run, todo):
+                if verbose and out.strip():
+                    print(out)
     if force or _newer(objs, LIB_PATH):
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB_PATH] + objs
         if verbose:
