@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8192, help="windows per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="windows per GPU per step (8192; 1024 with --train)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--traj", action="store_true",
                     help="config 3: camera-trajectory conditioned input (46 ch) with the "
@@ -53,10 +53,16 @@ def parse():
     ap.add_argument("--stream", action="store_true",
                     help="config 5: causal streaming, one frame per step, hipGraph replay "
                          "(use --dtype fp16 and a large --steps)")
+    ap.add_argument("--train", action="store_true",
+                    help="training iteration (f32): TemporalModel train mode + backward + Adam; "
+                         "--batch defaults to 1024 windows (run.py's batch_size)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="approximate CPU-baseline sample duration (0 disables)")
     ap.add_argument("--parity-windows", type=int, default=32)
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 1024 if args.train else 8192
+    return args
 
 
 def synth_windows(B, T, jin, seed, device):
@@ -173,6 +179,128 @@ def stream_main(args, world, rank, dev):
 RF_FULL = 243
 
 
+def train_flop_per_window(T, fw=FW, cin=2 * JOINTS, channels=CHANNELS, jout=JOINTS):
+    """Algorithmic FLOP of one training iteration of the dilated TemporalModel on one
+    window of T frames: forward convs + weight gradients + input gradients (none for the
+    expand conv, whose input is data).  2 x MACs, BN/ReLU/dropout/Adam excluded."""
+    L = T - (fw[0] - 1)
+    fwd = wg = dg = 2 * L * channels * cin * fw[0]
+    wg = fwd
+    dg = 0
+    dil = fw[0]
+    for w in fw[1:]:
+        L = L - (w - 1) * dil
+        k = 2 * L * channels * channels * w + 2 * L * channels * channels
+        fwd += k
+        wg += k
+        dg += k
+        dil *= w
+    s = 2 * L * channels * jout * 3
+    return fwd + s, wg + s, dg + s
+
+
+def train_main(args, world, rank, dev):
+    """Training throughput: the reference's iteration (run.py:451-487) — TemporalModel
+    (dilated, 3,3,3,3,3, 1024 ch, dropout 0.25) in train mode on B windows of 243 frames
+    (run.py:666: ChunkedGenerator(batch_size // stride) with stride 1), mpjpe, backward,
+    Adam(amsgrad) (run.py:662) — f32 on the native trainer.  N > 1 ranks: data-parallel,
+    gradients averaged with one all_reduce per step (RCCL)."""
+    from common.models.TemporalModel import TemporalModel
+    from vp3d_amd import synth
+    from vp3d_amd.train import Adam
+
+    model = TemporalModel(JOINTS, 2, JOINTS, FW, channels=CHANNELS, dropout=0.25)
+    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.cuda().train()
+    opt = Adam(model.parameters(), lr=1e-3, amsgrad=True)
+    RF = model.receptive_field()
+    B = args.batch
+    x = synth_windows(B, RF, JOINTS, 1000 + rank, dev)
+    tgt = (torch.randn((B, 1, JOINTS, 3), device=dev) * 0.2).contiguous()
+    params = [p for p in model.parameters()]
+    flat = None
+    if world > 1:
+        flat = torch.empty(sum(p.numel() for p in params), device=dev)
+
+    def step():
+        y = model(x)
+        loss = torch.mean(torch.norm(y - tgt, dim=-1))
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        if world > 1:
+            # one bucket: every gradient in one RCCL all_reduce (68 MB)
+            torch.cat([p.grad.reshape(-1) for p in params], out=flat)
+            dist.all_reduce(flat)
+            flat.div_(world)
+            o = 0
+            for p in params:
+                p.grad.copy_(flat[o:o + p.numel()].view_as(p))
+                o += p.numel()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        return
+    fwd, wg, dg = train_flop_per_window(RF)
+    flop_step = (fwd + wg + dg) * B
+    windows_s = world * B * args.steps / dt
+    out = {
+        "metric": "training windows/sec (TemporalModel 243-frame RF, 17 joints, 1024ch, f32)",
+        "value": round(windows_s, 2), "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded windows, counter-hash weights)",
+        "config": {"workload": "training iteration run.py:451-487: TemporalModel train mode (BN batch stats, "
+                               "dropout 0.25) + mpjpe + backward + Adam(amsgrad)",
+                   "windows_per_gpu": B, "global_batch": B * world,
+                   "parallelism": f"dp{world}" + (" (gradient all_reduce, RCCL)" if world > 1 else "")},
+        "flop_per_window": fwd + wg + dg,
+        "tflops_effective": round(flop_step * world * args.steps / dt / 1e12, 2),
+        "loss_last": float(loss.item()),
+    }
+    if args.cpu_seconds > 0:
+        out["cpu_baseline"] = train_cpu_baseline(sd, RF, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+def train_cpu_baseline(sd, RF, seconds):
+    """The oracle's training iteration (reference op sequence, torch-CPU autograd + Adam) on
+    a bounded sample: batches of 8 windows until ~`seconds` elapse."""
+    from oracle.train_ref import TrainLoop
+    threads = torch.get_num_threads()
+    loop = TrainLoop(sd, FW, lr=1e-3, amsgrad=True)
+    rng = np.random.default_rng(0)
+    Bc = 8
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        x = (rng.standard_normal((Bc, RF, JOINTS, 2)) * 0.3).astype(np.float32)
+        tg = (rng.standard_normal((Bc, 1, JOINTS, 3)) * 0.2).astype(np.float32)
+        loop.step(x, tg)
+        n += Bc
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": f"{n} windows (batches of {Bc}, dropout 0) through the oracle's training iteration "
+                      f"(oracle/train_ref.py: torch-CPU autograd + Adam) in {dt:.1f} s"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,8 +310,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if args.stream:
-        stream_main(args, world, rank, dev)
+    if args.stream or args.train:
+        (train_main if args.train else stream_main)(args, world, rank, dev)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()

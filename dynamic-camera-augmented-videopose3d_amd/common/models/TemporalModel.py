@@ -16,9 +16,13 @@ Eval-mode forward on a HIP device runs the MI355X kernels of libvp3d.so
 epilogue applies the folded BatchNorm, ReLU, dropout (identity in eval) and the
 residual slice-add.  A CPU input in eval mode raises — there is no fallback.
 
-Train mode (batch statistics, dropout, autograd) is not part of the MI355X hot
-path; it evaluates the module graph with stock torch
-ops so that the reference's training loop keeps working unchanged.
+Train mode runs the native training step too
+(include/vp3d.h ``vp3d_train_forward`` / ``vp3d_train_backward`` through the
+autograd node ``vp3d_amd.train.TrainStep``): BatchNorm batch statistics with the
+running-stat update, ReLU, dropout (counter-hash masks), the residual add and the
+backward of every layer, all in f32 on the device, so the reference's training loop
+(``loss.backward()``, ``optimizer.step()``) runs unchanged.  A CPU input raises in
+train mode as in eval mode.
 
 Precision: fp32 by default (exact f32 MFMA, the parity path);
 ``model.set_compute_dtype('bf16' | 'fp16')`` selects the 16-bit MFMA path.
@@ -27,7 +31,8 @@ import torch
 import torch.nn as nn
 
 from vp3d_amd import _native as _N
-from vp3d_amd.lifter import NativeLifter
+from vp3d_amd.lifter import NativeLifter, weight_order
+from vp3d_amd.train import NativeTrainer, TrainStep
 
 __all__ = ["TemporalModelBase", "TemporalModel", "TemporalModelOptimized1f"]
 
@@ -87,6 +92,7 @@ class TemporalModelBase(nn.Module):
         self.compute_dtype = 'fp32'
         self._lifter = None
         self._lifter_key = None
+        self._trainer = None
 
     def _build_stack(self, strided, dense):
         pad, shift, blocks = _plan_blocks(self.filter_widths, self.causal, strided, dense)
@@ -162,33 +168,64 @@ class TemporalModelBase(nn.Module):
         self._lifter_key = key
         return self._lifter
 
+    def native_trainer(self, device) -> NativeTrainer:
+        """The NativeTrainer (train-mode forward/backward engine) for `device`."""
+        device = torch.device(device)
+        if self._trainer is None or self._trainer.device != device:
+            self._trainer = NativeTrainer(self.num_joints_in, self.in_features, self.num_joints_out,
+                                          self.filter_widths, self.causal, self.channels, self.dense,
+                                          self._variant, device, bn_eps=self.expand_bn.eps)
+        return self._trainer
+
     def forward(self, x):
         assert len(x.shape) == 4
         assert x.shape[-2] == self.num_joints_in
         assert x.shape[-1] == self.in_features
-        if self.training:
-            return self._train_graph(x)
         if not x.is_cuda:
             raise RuntimeError(
-                "vp3d: eval-mode forward needs a HIP device tensor (no CPU fallback); "
+                "vp3d: the lifter runs on the MI355X kernels only (no CPU fallback); "
                 "call model.cuda() and pass x.cuda()")
+        if self.training:
+            return self._train_forward(x)
         return self.native_lifter(x.device).forward(x, self.compute_dtype)
 
-    def _train_graph(self, x):
-        """Training-mode graph with torch ops (channel-first, as the reference)."""
-        B, T = x.shape[0], x.shape[1]
-        h = x.reshape(B, T, -1).transpose(1, 2)
-        h = self.drop(self.relu(self.expand_bn(self.expand_conv(h))))
-        for i, blk in enumerate(self._blocks):
-            start = blk["res_start"]
-            if blk["res_step"] == 1:
-                res = h[:, :, start:h.shape[2] - blk["res_trim"]]
-            else:
-                res = h[:, :, start::blk["res_step"]]
-            h = self.drop(self.relu(self.layers_bn[2 * i](self.layers_conv[2 * i](h))))
-            h = res + self.drop(self.relu(self.layers_bn[2 * i + 1](self.layers_conv[2 * i + 1](h))))
-        out = self.shrink(h).transpose(1, 2)
-        return out.reshape(B, -1, self.num_joints_out, 3)
+    def _train_forward(self, x):
+        """Train-mode forward through the native trainer (TemporalModel.py:62-76, :126-138 /
+        :188-198 with BatchNorm1d in training mode and nn.Dropout active)."""
+        bns = [self.expand_bn, *self.layers_bn]
+        momentum = bns[0].momentum
+        if any(bn.momentum != momentum for bn in bns):
+            raise NotImplementedError("vp3d: per-layer BatchNorm momenta differ (set_bn_momentum sets one)")
+        if any(not bn.track_running_stats or not bn.training for bn in bns):
+            raise NotImplementedError("vp3d: train mode needs every BatchNorm training with running stats")
+        # BatchNorm1d.forward: count the batch; cumulative average when momentum is None
+        for bn in bns:
+            bn.num_batches_tracked.add_(1)
+        factor = (1.0 / float(bns[0].num_batches_tracked.item())) if momentum is None else momentum
+        state = self.state_dict(keep_vars=True)
+        tensors = [state[k] for k in weight_order(len(self.filter_widths))]
+        for t in tensors:
+            if t.device != x.device or t.dtype != torch.float32 or not t.is_contiguous():
+                raise RuntimeError("vp3d: parameters must be contiguous float32 tensors on the input's device")
+        trainable = tuple(isinstance(t, nn.Parameter) and t.requires_grad for t in tensors)
+        trainer = self.native_trainer(x.device)
+        T_out = self._out_frames(int(x.shape[1]))
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self.drop.p > 0 else 0
+        x = x.contiguous().float()
+        return TrainStep.apply(trainer, float(self.drop.p), float(factor), seed, T_out, trainable, x, *tensors)
+
+    def _out_frames(self, T):
+        """Output frames for T input frames (the conv length rules of TemporalModel.py)."""
+        w0 = self.filter_widths[0]
+        strided = self._variant == _N.VARIANT_STRIDED_1F
+        L = (T - w0) // w0 + 1 if strided else T - (w0 - 1)
+        for blk in self._blocks:
+            span = (blk["kernel"] - 1) * blk["dilation"] + 1
+            L = (L - span) // blk["stride"] + 1 if L >= span else 0
+        if L < 1:
+            raise RuntimeError(f"input of {T} frames is shorter than the receptive field "
+                               f"{self.receptive_field()}")
+        return L
 
 
 class TemporalModel(TemporalModelBase):

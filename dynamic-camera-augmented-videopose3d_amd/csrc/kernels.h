@@ -135,4 +135,54 @@ hipError_t launch_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_
 hipError_t launch_pose_metrics(const float* pred, const float* target, int64_t n_frames, int J, double* acc,
                                hipStream_t s);
 
+// ---- training step (train.hip, vp3d_train.cpp) ----
+// weight gradient of one conv: part[s][n][k] over row splits s (TN GEMM over rows)
+struct WgradParams {
+    const float* dZ;   // output-gradient rows; row of (b, t) = b*dz_T + t + dz_off, ldz floats each
+    int ldz, dz_T, dz_off;
+    const float* X;    // layer input rows (cin floats); tap row = b*T_in + t*stride + tap*dil
+    int cin, T_in, stride, dil, T_out;
+    int64_t M;         // B * T_out
+    int N, K;          // cout, taps * cin
+    int64_t rows_per_split;
+    float* part;       // [S][N][K]
+};
+constexpr int kMaxAdamTensors = 64;
+struct AdamList {
+    float* param[kMaxAdamTensors];
+    const float* grad[kMaxAdamTensors];
+    float* exp_avg[kMaxAdamTensors];
+    float* exp_avg_sq[kMaxAdamTensors];
+    float* max_exp_avg_sq[kMaxAdamTensors];
+    int64_t numel[kMaxAdamTensors];
+    int block_start[kMaxAdamTensors + 1];  // 1024 elements per block
+    int n;
+};
+struct AdamHyper {
+    float lerp_w, beta2, one_minus_beta2, bc2_sqrt, eps, neg_step_size, weight_decay;
+    int amsgrad;
+};
+int64_t train_reduce_part_doubles(int64_t M, int C);
+// mode 0: forward [cout][k*cin+c]; 1: flipped-tap dgrad [cin][(taps-1-k)*cout+o]; 2: [k*cin+c][cout]
+hipError_t launch_pack_weights(const float* w, int cout, int cin, int taps, int mode, int Kp, float* out,
+                               hipStream_t s);
+hipError_t launch_bn_train_stats(const float* Z, int64_t M, int C, double* part, const float* gamma,
+                                 const float* beta, float eps, double momentum, float* running_mean,
+                                 float* running_var, float* mean, float* invstd, float* alpha, float* shift,
+                                 hipStream_t s);
+hipError_t launch_bn_act_fwd(const float* Z, int64_t M, int C, const float* alpha, const float* shift, float p,
+                             uint64_t seed, int layer, const float* R, int T_out, int R_T, int R_stride, int R_off,
+                             float* Y, hipStream_t s);
+hipError_t launch_bn_train_backward(const float* dO, const float* Z, int64_t M, int C, const float* gamma,
+                                    const float* alpha, const float* shift, const float* mean, const float* invstd,
+                                    float p, uint64_t seed, int layer, double* part, float* coef, float* dgamma,
+                                    float* dbeta, int T_out, int dz_T, int dz_off, float* dZ, hipStream_t s);
+hipError_t launch_colsum(const float* D, int64_t M, int C, int ld, double* part, float* out, hipStream_t s);
+hipError_t launch_res_grad_add(float* dIn, const float* dOut, int64_t M, int C, int T_out, int T_in, int rs, int ro,
+                               hipStream_t s);
+int wgrad_splits(int64_t M, int N, int K, int64_t max_part_floats);
+hipError_t launch_wgrad(const WgradParams& p, int S, int taps, float* dW, hipStream_t s);
+hipError_t launch_adam(const AdamList& L, const AdamHyper& hp, hipStream_t s);
+hipError_t launch_dropout_mask(uint64_t seed, float p, int layer, int64_t n, uint8_t* out, hipStream_t s);
+
 }  // namespace vp3d

@@ -48,6 +48,8 @@ EXPORTS = [
     "vp3d_stream_create", "vp3d_stream_reset", "vp3d_stream_io", "vp3d_stream_step",
     "vp3d_stream_frames_seen", "vp3d_stream_graph_capture", "vp3d_stream_graph_launch",
     "vp3d_stream_destroy",
+    "vp3d_trainer_create", "vp3d_trainer_destroy", "vp3d_train_forward", "vp3d_train_backward",
+    "vp3d_train_dropout_mask", "vp3d_train_layer_rows", "vp3d_adam_step",
 ]
 
 
@@ -105,6 +107,17 @@ _SIGNATURES = {
     "vp3d_stream_graph_capture": (_int, [_vp, _vp, _int]),
     "vp3d_stream_graph_launch": (_int, [_vp, _vp]),
     "vp3d_stream_destroy": (_int, [_vp]),
+    "vp3d_trainer_create": (_int, [ctypes.POINTER(vp3d_cfg), ctypes.POINTER(_vp)]),
+    "vp3d_trainer_destroy": (_int, [_vp]),
+    "vp3d_train_forward": (_int, [_vp, ctypes.POINTER(_vp), _int, _vp, _int, _int, ctypes.c_float,
+                                  ctypes.c_double, ctypes.c_uint64, _vp, _vp]),
+    "vp3d_train_backward": (_int, [_vp, ctypes.POINTER(_vp), _int, _vp, ctypes.POINTER(_vp), _vp]),
+    "vp3d_train_dropout_mask": (_int, [_vp, _int, _i64, _vp, _vp]),
+    "vp3d_train_layer_rows": (_i64, [_vp, _int]),
+    "vp3d_adam_step": (_int, [_int, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                              ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
+                              ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                              ctypes.c_double, _i64, _int, _vp]),
     "vp3d_last_error": (ctypes.c_char_p, []),
     "vp3d_abi_version": (_int, []),
 }

@@ -167,6 +167,65 @@ int vp3d_stream_graph_capture(vp3d_stream* s, void* stream, int steps);
 int vp3d_stream_graph_launch(vp3d_stream* s, void* stream);
 int vp3d_stream_destroy(vp3d_stream* s);
 
+/* ---- training step (run.py:451-487, :662) ----
+ * The reference trains TemporalModel in train mode: BatchNorm1d on batch
+ * statistics with a running-stat update (TemporalModel.py:117,119; momentum
+ * decayed per epoch by set_bn_momentum :35-38, run.py:553-556), ReLU, Dropout
+ * (:130-137), the residual add, then loss.backward() and
+ * optim.Adam(amsgrad=True).step().  A trainer runs that forward/backward on the
+ * device in f32.  Parameters stay in caller-owned device memory (the
+ * nn.Module's own tensors) and are passed per call as a table of device
+ * pointers in state_dict order — the same order and count as vp3d_create's
+ * `weights` (vp3d_weight_count): conv weight, then BN weight / bias /
+ * running_mean / running_var per conv, shrink weight and bias.  Dropout masks
+ * come from a counter-based hash of (seed, layer, element), regenerated in the
+ * backward rather than stored (vp3d_train_dropout_mask exports them). */
+typedef struct vp3d_trainer vp3d_trainer;
+
+int vp3d_trainer_create(const vp3d_cfg* cfg, vp3d_trainer** out);
+int vp3d_trainer_destroy(vp3d_trainer* t);
+
+/* Train-mode forward (TemporalModelBase.forward in train mode, TemporalModel.py:62-76).
+ * params: host array of n_params DEVICE pointers (state_dict order); the BN
+ * running_mean / running_var entries are updated in place with `momentum`
+ * (BatchNorm1d.momentum).  x: device f32 (B, T, J_in, F); y: device f32
+ * (B, vp3d_out_frames(T), J_out, 3).  dropout_p: nn.Dropout p; seed: mask seed.
+ * The activations the backward needs are kept inside the trainer until the next
+ * forward. */
+int vp3d_train_forward(vp3d_trainer* t, float* const* params, int n_params, const float* x, int B, int T,
+                       float dropout_p, double momentum, uint64_t seed, float* y, void* stream);
+
+/* Backward of the latest vp3d_train_forward (same params, which must not have
+ * changed in between).  dy: device f32 like y.  grads: host array of n_params
+ * device pointers, state_dict order; each trainable entry receives its gradient
+ * (overwritten, torch layout); running-stat entries are ignored and may be NULL.
+ * The input gradient is not formed (the 2D keypoints are data, run.py:458). */
+int vp3d_train_backward(vp3d_trainer* t, float* const* params, int n_params, const float* dy,
+                        float* const* grads, void* stream);
+
+/* The dropout keep mask (1 = kept) of conv layer `layer` (0 = expand, then the
+ * block convs in order) for the latest forward: n_elems = rows * channels of that
+ * layer's output, row-major (b, t, c).  Test hook for the parity tests. */
+int vp3d_train_dropout_mask(vp3d_trainer* t, int layer, int64_t n_elems, uint8_t* out, void* stream);
+
+/* Row count (B * frames) of conv layer `layer`'s output in the latest forward, or -1. */
+int64_t vp3d_train_layer_rows(const vp3d_trainer* t, int layer);
+
+/* One Adam step over n tensors (torch.optim.Adam, _single_tensor_adam; run.py:662
+ * builds it with amsgrad=True): for each i, with g = grad (+ weight_decay * param),
+ *   exp_avg = lerp(exp_avg, g, 1 - beta1)   (as fma, like ATen's vectorised lerp)
+ *   exp_avg_sq = fma((1 - beta2) * g, g, exp_avg_sq * beta2)
+ *   max_exp_avg_sq = max(max_exp_avg_sq, exp_avg_sq)                    (amsgrad)
+ *   param += -lr / (1 - beta1^step) * exp_avg / (sqrt(max_exp_avg_sq or exp_avg_sq)
+ *                                                / sqrt(1 - beta2^step) + eps)
+ * `step` is the already-incremented step count.  All arrays are host arrays of
+ * device pointers / element counts; max_exp_avg_sq entries may be NULL without
+ * amsgrad.  n <= 64 per call. */
+int vp3d_adam_step(int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, float* const* max_exp_avg_sq, const int64_t* numel, double lr,
+                   double beta1, double beta2, double eps, double weight_decay, int64_t step, int amsgrad,
+                   void* stream);
+
 /* ---- on-device input path (common/camera.py, common/generators.py) ---- */
 
 /* normalize_screen_coordinates (camera.py:14-18): out = X/w*2 - [1, h/w] for

@@ -246,8 +246,61 @@ def run_eval_golden():
                                                            subjects=3, actions=3, frames=200))))
 
 
+def train_case(name, strided, fw, B, T, causal=False, channels=64, dense=False, seed=0, steps=2):
+    """Two reference training iterations (run.py:451-487 with TemporalModel in train mode,
+    dropout 0): forward with BatchNorm batch statistics, mpjpe, backward,
+    optim.Adam(amsgrad=True).step() (run.py:662).  Stores inputs, weights and per step
+    the output, loss, every gradient, the running statistics and the updated weights."""
+    m, sd, keys = build_ref_model(strided, fw, causal, channels, dense=dense, seed=seed)
+    if strided:
+        m = ref_tm.TemporalModelOptimized1f(17, 2, 17, list(fw), causal=causal, channels=channels,
+                                            dropout=0.0)
+    else:
+        m = ref_tm.TemporalModel(17, 2, 17, list(fw), causal=causal, channels=channels, dense=dense,
+                                 dropout=0.0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.train()
+    m.set_bn_momentum(0.1)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, amsgrad=True)
+    arrays = {}
+    for k, v in sd.items():
+        arrays["w/" + k] = v
+    T_out = None
+    for it in range(steps):
+        x = synth.normalized_windows(seed + 10 + it, name, B, T)
+        y = m(torch.from_numpy(x))
+        T_out = y.shape[1]
+        tgt = synth.normal(seed + 20 + it, name + "/target", (B, T_out, 17, 3), std=0.2).astype(np.float32)
+        loss = ref_loss.mpjpe(y, torch.from_numpy(tgt))
+        opt.zero_grad()
+        loss.backward()
+        arrays[f"s{it}/x"] = x
+        arrays[f"s{it}/target"] = tgt
+        arrays[f"s{it}/y"] = y.detach().numpy()
+        arrays[f"s{it}/loss"] = np.array(loss.item(), dtype=np.float32)
+        for k, p in m.named_parameters():
+            arrays[f"s{it}/grad/{k}"] = p.grad.numpy().copy()
+        opt.step()
+        for k, v in m.state_dict().items():
+            arrays[f"s{it}/after/{k}"] = v.numpy().copy()
+    meta = dict(strided=strided, fw=list(fw), causal=causal, channels=channels, dense=dense, seed=seed,
+                B=B, T=T, T_out=int(T_out), steps=steps, lr=1e-3, amsgrad=True, momentum=0.1,
+                keys=[k for k, _ in keys])
+    arrays["meta"] = np.array(json.dumps(meta))
+    save(name, **arrays)
+
+
+def train_goldens():
+    F3 = (3, 3, 3)
+    train_case("train_dilated_c64", False, F3, 6, 31)           # chunk of 5 output frames
+    train_case("train_opt1f_c64", True, F3, 8, 27)
+    train_case("train_causal_c64", False, (3, 5, 3), 3, 80, causal=True)
+    train_case("train_dense_c32", False, F3, 2, 40, channels=32, dense=True)
+
+
 GROUPS = {"run_eval": run_eval_golden, "model": model_goldens, "generator": generator_goldens,
-          "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens}
+          "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens,
+          "train": train_goldens}
 
 if __name__ == "__main__":
     # python make_golden.py [group ...]  (default: every group); the manifest is merged

@@ -68,22 +68,6 @@ def test_dropin_module_structure(name):
     assert pad == meta["pad"] and shift == meta["causal_shift"]
 
 
-def test_dropin_train_mode_matches_reference_graph():
-    """Train-mode graph (torch ops, not the MI355X path) equals the oracle in eval
-    semantics when dropout is 0 and BN uses running stats (eval-mode BN modules)."""
-    from common.models.TemporalModel import TemporalModel
-    g = load("small_causal_c64")
-    meta = json.loads(str(g["meta"]))
-    m = TemporalModel(17, 2, 17, meta["fw"], causal=True, channels=64, dropout=0.0)
-    m.load_state_dict({k: torch.from_numpy(v) for k, v in case_weights(g, meta).items()})
-    m.train()
-    for bn in [m.expand_bn, *m.layers_bn]:
-        bn.eval()
-    with torch.no_grad():
-        y = m(torch.from_numpy(g["x"])).numpy()
-    np.testing.assert_allclose(y, g["y"], atol=1e-6)
-
-
 def test_receptive_fields():
     assert receptive_field([3, 3, 3, 3, 3]) == 243
     assert receptive_field([3, 3, 3]) == 27
