@@ -5,7 +5,7 @@ options and defaults (-d/--dataset, -k/--keypoints, --subjects-test, -a/--action
 -c/--checkpoint, --evaluate, --by-subject, --use-model, -b/--batch-size,
 -s/--stride, --fcn-architecture, --causal, -ch/--channels, --fcn-dropout,
 --dense, --disable-optimizations, --downsample).  The other model families'
-and the trainer's flags are accepted for command-line compatibility and ignored.
+and the trainer's flags (-e, -lr, -lrd, -r, --checkpoint-frequency, --no-eval) drive the training loop of run.py; the rest are accepted for compatibility and ignored.
 Added: --compute-dtype, --trust-checkpoint and the --synthetic-* data options.
 """
 import argparse

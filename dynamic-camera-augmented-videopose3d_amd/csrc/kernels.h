@@ -129,6 +129,8 @@ hipError_t launch_pack_rows(const float* x, int M, int T_out, int T_in, int stri
                             int K, int Kp, void* out, bool bf16, hipStream_t s);
 hipError_t launch_mpjpe_accumulate(const float* pred, const float* target, int64_t n,
                                    double* acc, hipStream_t s);
+hipError_t launch_mpjpe_backward(const float* pred, const float* target, int64_t n, const float* grad_loss,
+                                 float* grad_pred, hipStream_t s);
 hipError_t launch_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_cam, const float* params,
                                 bool linear, float* out, hipStream_t s);
 // metrics.hip: MPJPE / P-MPJPE / N-MPJPE / MPJVE partial sums per (n_frames, J, 3) pair

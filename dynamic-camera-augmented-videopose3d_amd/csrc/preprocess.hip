@@ -155,6 +155,26 @@ __global__ void mpjpe_kernel(const float* __restrict__ pred, const float* __rest
     }
 }
 
+// Gradient of mpjpe = mean ||pred - target|| (loss.py:11-17) wrt pred, the backward of
+// torch.mean(torch.norm(d, dim=-1)): g/n * d / ||d|| per point (0 where ||d|| == 0, as
+// torch's norm backward masks it).  g = *grad_loss (device scalar).
+__global__ void mpjpe_backward_kernel(const float* __restrict__ pred, const float* __restrict__ target,
+                                      int64_t n, const float* __restrict__ grad_loss,
+                                      float* __restrict__ grad_pred) {
+    const float gn = grad_loss[0] / (float)n;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float dx = pred[3 * i] - target[3 * i];
+        const float dy = pred[3 * i + 1] - target[3 * i + 1];
+        const float dz = pred[3 * i + 2] - target[3 * i + 2];
+        const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
+        const float sc = nrm > 0.f ? gn / nrm : 0.f;
+        grad_pred[3 * i] = dx * sc;
+        grad_pred[3 * i + 1] = dy * sc;
+        grad_pred[3 * i + 2] = dz * sc;
+    }
+}
+
 // H36M camera projection of camera-space points, one thread per point; camera of
 // point i = i / pts_per_cam, params [f(2), c(2), k(3), p(2)].  The torch-float32
 // op order of camera.py:59-67: XX = clamp(X_xy / X_z, -1, 1); r2 = (0 + x^2) + y^2;
@@ -229,6 +249,14 @@ hipError_t launch_gather_windows(const float* kps, int f2, const float* cams,
     const int64_t total = (int64_t)B * window * (f2 + (cams ? 12 : 0));
     hipLaunchKernelGGL(gather_windows_kernel, grid_for(total, 4), dim3(kThreads), 0, s, kps, f2,
                        cams, seq_off, seq_len, pairs, B, window, pad + shift, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_mpjpe_backward(const float* pred, const float* target, int64_t n, const float* grad_loss,
+                                 float* grad_pred, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mpjpe_backward_kernel, grid_for(n, 1), dim3(kThreads), 0, s, pred, target, n, grad_loss,
+                       grad_pred);
     return hipGetLastError();
 }
 

@@ -925,6 +925,14 @@ int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_poin
     return VP3D_OK;
 }
 
+int vp3d_mpjpe_backward(const float* pred, const float* target, int64_t n_points, const float* grad_loss,
+                        float* grad_pred, void* stream) {
+    if (n_points < 0 || (n_points > 0 && (!pred || !target || !grad_loss || !grad_pred)))
+        return fail(VP3D_ERR_ARG, "bad pointer");
+    HIP_TRY(launch_mpjpe_backward(pred, target, n_points, grad_loss, grad_pred, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
 
 int vp3d_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_cam, const float* params, int32_t linear,
                        float* out, void* stream) {

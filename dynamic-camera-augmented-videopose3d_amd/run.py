@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Evaluation driver of the temporal-lifter path (drop-in for the FCN branch of the
-reference's run.py --evaluate, run.py:290-309 model build, :400-417 device and
-checkpoint, :862-995 per-action evaluation).
+"""Training and evaluation driver of the temporal-lifter path (drop-in for the FCN
+branch of the reference's run.py: :290-309 model build, :400-417 device and
+checkpoint, :424-590 the training loop, :653-673 its entry, :862-995 per-action
+evaluation).
 
+    python run.py -e 60 -c checkpoint --subjects-train S1,S2 --subjects-test S3   # train
     python run.py --evaluate synthetic --fcn-architecture 3,3,3 --subjects-test '*'
     python run.py --evaluate epoch_60.bin -c checkpoint --causal --compute-dtype bf16
 
@@ -20,6 +22,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
+
+import time  # noqa: E402
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -75,15 +79,16 @@ def run_evaluation(data, actions, make_generator, model_fn, metrics, action_filt
     return {"per_action": per_action, "summary": summary, "pmcc": pmcc}
 
 
-def build_model(args, J):
+def build_model(args, J, announce=True):
     from common.models.TemporalModel import TemporalModel
     from vp3d_amd import synth
     fw = [int(x) for x in args.fcn_architecture.split(",")]
     jin = J + 6 if args.trajectory else J
     model = TemporalModel(jin, 2, J, filter_widths=fw, causal=args.causal, dropout=args.fcn_dropout,
                           channels=args.channels, dense=args.dense)
-    print('INFO: Receptive field: {} frames'.format(model.receptive_field()))
-    print('INFO: Trainable parameter count:', sum(p.numel() for p in model.parameters()))
+    if announce:
+        print('INFO: Receptive field: {} frames'.format(model.receptive_field()))
+        print('INFO: Trainable parameter count:', sum(p.numel() for p in model.parameters()))
     if args.evaluate == "synthetic" or not args.evaluate:
         sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()],
                                      seed=args.seed)
@@ -94,6 +99,126 @@ def build_model(args, J):
         ckpt = torch.load(path, map_location="cpu", weights_only=not args.trust_checkpoint)
         model.load_state_dict(ckpt["model_pos"])
     return model
+
+
+def fetch(data, subjects, action_filter=None):
+    """(cameras, poses_3d, poses_2d) lists of the given subjects (run.py:140-182)."""
+    cams, p3d, p2d = [], [], []
+    for s in subjects:
+        for a in data[s]:
+            if action_filter is not None and not any(a.startswith(f) for f in action_filter):
+                continue
+            cams.append(data[s][a]["cameras"])
+            p3d.append(data[s][a]["positions_3d"])
+            p2d.append(data[s][a]["keypoints"])
+    return cams, p3d, p2d
+
+
+def train(args, n_epochs, train_generator, test_generator, model_pos_train, model_pos, optimizer,
+          lr, lr_decay, save_state=True, resume=None, log=print):
+    """The reference's epoch loop (run.py:424-590) for the temporal FCN: per batch the
+    train-mode forward, mpjpe, backward and Adam step on the MI355X; per epoch the
+    evaluation of the copied weights on the test generator, the exponential lr decay, the
+    BatchNorm momentum decay 0.1 -> 0.001 and the checkpoint.  Returns the per-epoch
+    (train, valid) losses in metres and the best validation error."""
+    from common.loss import mpjpe
+
+    losses_train, losses_valid = [], []
+    epoch = 0
+    initial_momentum, final_momentum = 0.1, 0.001
+    if resume is not None:  # run.py:436-445
+        epoch = resume["epoch"]
+        if resume.get("optimizer") is not None:
+            optimizer.load_state_dict(resume["optimizer"])
+            train_generator.set_random_state(resume["random_state"])
+        lr = resume["lr"]
+    best = float("inf")
+    while epoch < n_epochs:
+        t0 = time.time()
+        sum_train = 0.0
+        N = 0
+        model_pos_train.train()
+        for batch_cam, batch_3d, batch_2d in train_generator.next_epoch():
+            pred = model_pos_train(batch_2d)
+            loss = mpjpe(pred, batch_3d)
+            optimizer.zero_grad()
+            loss.backward()
+            optimizer.step()
+            n = batch_3d.shape[0] * batch_3d.shape[1]
+            sum_train += n * loss.item()
+            N += n
+        losses_train.append(sum_train / N)
+        with torch.no_grad():
+            model_pos.load_state_dict(model_pos_train.state_dict())
+            model_pos.eval()
+            if not args.no_eval:
+                sum_valid = 0.0
+                N = 0
+                for batch_cam, batch_3d, batch_2d, _ in test_generator():
+                    loss = mpjpe(model_pos(batch_2d), batch_3d)
+                    n = batch_3d.shape[0] * batch_3d.shape[1]
+                    sum_valid += n * loss.item()
+                    N += n
+                losses_valid.append(sum_valid / N)
+                best = min(best, losses_valid[-1])
+        elapsed = (time.time() - t0) / 60
+        if args.no_eval:
+            log('[%d] time %.2f lr %f 3d_train %f' % (epoch + 1, elapsed, lr, losses_train[-1] * 1000))
+        else:
+            log('[%d] time %.2f lr %f 3d_train %f 3d_valid %f' % (
+                epoch + 1, elapsed, lr, losses_train[-1] * 1000, losses_valid[-1] * 1000))
+        lr *= lr_decay
+        for group in optimizer.param_groups:
+            group["lr"] *= lr_decay
+        epoch += 1
+        momentum = initial_momentum * np.exp(-epoch / args.epochs * np.log(initial_momentum / final_momentum))
+        model_pos_train.set_bn_momentum(momentum)
+        if save_state and epoch % args.checkpoint_frequency == 0:
+            os.makedirs(args.checkpoint, exist_ok=True)
+            path = os.path.join(args.checkpoint, 'epoch_{}.bin'.format(epoch))
+            log('Saving checkpoint to', path)
+            torch.save({'epoch': epoch, 'lr': lr, 'random_state': train_generator.random_state(),
+                        'optimizer': optimizer.state_dict(), 'model_pos': model_pos_train.state_dict()}, path)
+    return {"train": losses_train, "valid": losses_valid, "best_valid": best}
+
+
+def train_main(args, data):
+    """`run.py` without --evaluate (run.py:653-673): ChunkedGenerator batches of
+    batch_size // stride chunks of `stride` frames, Adam(lr, amsgrad=True), train()."""
+    from common.generators import ChunkedGenerator, UnchunkedGenerator
+    from vp3d_amd.train import Adam
+
+    subjects = list(data.keys())
+    subjects_train = subjects if args.subjects_train in (None, "*") else args.subjects_train.split(",")
+    subjects_test = subjects if args.subjects_test in (None, "*") else args.subjects_test.split(",")
+    action_filter = None if args.actions == "*" else args.actions.split(",")
+    print("Training Subjects: ", ", ".join(subjects_train))
+    print("Test Subjects: ", ", ".join(subjects_test))
+    model_pos_train = build_model(args, args.joints).cuda()
+    model_pos = build_model(args, args.joints, announce=False).cuda()
+    pad = (model_pos.receptive_field() - 1) // 2
+    causal_shift = pad if args.causal else 0
+    cams_tr, p3d_tr, p2d_tr = fetch(data, subjects_train, action_filter)
+    cams_te, p3d_te, p2d_te = fetch(data, subjects_test, action_filter)
+    resume = None
+    if args.resume:
+        path = os.path.join(args.checkpoint, args.resume)
+        print('Loading checkpoint', path)
+        # a run.py checkpoint holds the generator's numpy RandomState (run.py:566)
+        resume = torch.load(path, map_location="cpu", weights_only=False)
+        model_pos_train.load_state_dict(resume["model_pos"])
+    optimizer = Adam(model_pos_train.parameters(), lr=args.learning_rate, amsgrad=True)
+    train_generator = ChunkedGenerator(args.batch_size // args.stride, cams_tr, p3d_tr, p2d_tr, args.stride,
+                                       pad=pad, causal_shift=causal_shift, shuffle=True,
+                                       trajectory=args.trajectory)
+
+    def test_generator():
+        return UnchunkedGenerator(cams_te, p3d_te, p2d_te, pad=pad, causal_shift=causal_shift,
+                                  trajectory=args.trajectory).next_epoch()
+
+    print('INFO: Training on {} frames'.format(sum(p.shape[0] for p in p2d_tr)))
+    return train(args, args.epochs, train_generator, test_generator, model_pos_train, model_pos, optimizer,
+                 args.learning_rate, args.lr_decay, save_state=True, resume=resume)
 
 
 def main(argv=None):
@@ -107,6 +232,8 @@ def main(argv=None):
     if not torch.cuda.is_available():
         raise SystemExit("run.py evaluates on the MI355X (no CPU fallback)")
     data = synthetic_dataset(args)
+    if not args.evaluate:
+        return train_main(args, data)
     subjects = list(data.keys()) if args.subjects_test in (None, "*") else args.subjects_test.split(",")
     model = build_model(args, args.joints).cuda().eval()
     model.set_compute_dtype(args.compute_dtype)

@@ -49,7 +49,7 @@ EXPORTS = [
     "vp3d_stream_frames_seen", "vp3d_stream_graph_capture", "vp3d_stream_graph_launch",
     "vp3d_stream_destroy",
     "vp3d_trainer_create", "vp3d_trainer_destroy", "vp3d_train_forward", "vp3d_train_backward",
-    "vp3d_train_dropout_mask", "vp3d_train_layer_rows", "vp3d_adam_step",
+    "vp3d_train_dropout_mask", "vp3d_train_layer_rows", "vp3d_adam_step", "vp3d_mpjpe_backward",
 ]
 
 
@@ -97,6 +97,7 @@ _SIGNATURES = {
     "vp3d_world_to_camera": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),
     "vp3d_gather_windows": (_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
     "vp3d_mpjpe_accumulate": (_int, [_vp, _vp, _i64, _vp, _vp]),
+    "vp3d_mpjpe_backward": (_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "vp3d_pose_metrics": (_int, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "vp3d_project_to_2d": (_int, [_vp, _i64, _i64, _vp, _i32, _vp, _vp]),
     "vp3d_stream_create": (_int, [_vp, _int, ctypes.POINTER(_vp)]),

@@ -146,8 +146,38 @@ def pose_metrics(pred: torch.Tensor, target: torch.Tensor, acc: Optional[torch.T
     return acc
 
 
+class _MpjpeLoss(torch.autograd.Function):
+    """mpjpe as a differentiable loss (run.py:478-485): forward = the native reduction,
+    backward = vp3d_mpjpe_backward."""
+
+    @staticmethod
+    def forward(ctx, pred, target):
+        pred = pred.contiguous().float()
+        target = target.contiguous().float()
+        ctx.save_for_backward(pred, target)
+        acc = mpjpe_sums(pred, target)
+        return (acc[0] / acc[1]).float()
+
+    @staticmethod
+    def backward(ctx, grad):
+        pred, target = ctx.saved_tensors
+        g = torch.empty_like(pred)
+        grad = grad.contiguous().float()
+        with torch.cuda.device(pred.device):
+            N.check(N.load().vp3d_mpjpe_backward(pred.data_ptr(), target.data_ptr(), pred.numel() // 3,
+                                                 grad.data_ptr(), g.data_ptr(), _stream(pred)),
+                    "vp3d_mpjpe_backward")
+        return g, None
+
+
 def mpjpe(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-    """Mean per-joint position error (device scalar, float32 like torch.mean)."""
+    """Mean per-joint position error (device scalar, float32 like torch.mean);
+    differentiable with respect to `pred` (the training loss, run.py:478)."""
+    _require_cuda(pred, "pred")
+    _require_cuda(target, "target")
+    assert pred.shape == target.shape and pred.shape[-1] == 3
+    if pred.requires_grad and torch.is_grad_enabled():
+        return _MpjpeLoss.apply(pred, target)
     acc = mpjpe_sums(pred, target)
     return (acc[0] / acc[1]).float()
 

@@ -279,6 +279,13 @@ int vp3d_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_cam, cons
 int vp3d_mpjpe_accumulate(const float* pred, const float* target, int64_t n_points, double* acc,
                           void* stream);
 
+/* Gradient of the training loss mpjpe = mean ||pred - target|| (loss.py:11-17, run.py:478)
+ * with respect to pred: grad_pred = grad_loss[0] / n_points * (pred - target) / ||pred - target||
+ * per point (0 where the distance is 0).  grad_loss: device f32 scalar (the upstream
+ * gradient, 1 for loss.backward()); grad_pred: device f32 like pred. */
+int vp3d_mpjpe_backward(const float* pred, const float* target, int64_t n_points, const float* grad_loss,
+                        float* grad_pred, void* stream);
+
 /* Evaluation metrics of one sequence's predictions (run.py:732-750): partial sums of
  * MPJPE (loss.py:11-17), P-MPJPE (rigid alignment per frame, loss.py:29-68), N-MPJPE
  * (per-frame scale, loss.py:70-80) and MPJVE (first difference along frames,

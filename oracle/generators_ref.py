@@ -43,11 +43,18 @@ def edge_slice(arr, start, end):
 
 
 def chunked_batches(cams, poses_3d, poses_2d, batch_size, chunk_length, pad, causal_shift,
-                    shuffle=True, seed=1234):
+                    shuffle=True, seed=1234, random=None):
     """Yields (batch_cam, batch_3d, batch_2d) exactly as ChunkedGenerator.next_epoch does,
-    including the reuse of one float64 buffer per array (stale rows in the last batch)."""
-    pairs = (shuffled_pairs([p.shape[0] for p in poses_2d], chunk_length, seed) if shuffle
-             else np.array(chunk_pairs([p.shape[0] for p in poses_2d], chunk_length)))
+    including the reuse of one float64 buffer per array (stale rows in the last batch).
+    `random`: the generator's RandomState carried across epochs (generators.py:56, :85;
+    each epoch draws the next permutation from it); default a fresh RandomState(seed)."""
+    lengths = [p.shape[0] for p in poses_2d]
+    if not shuffle:
+        pairs = np.array(chunk_pairs(lengths, chunk_length))
+    elif random is not None:
+        pairs = random.permutation(chunk_pairs(lengths, chunk_length))
+    else:
+        pairs = shuffled_pairs(lengths, chunk_length, seed)
     L = chunk_length + 2 * pad
     bcam = np.empty((batch_size, L, 3, 4))
     b3d = np.empty((batch_size, chunk_length) + poses_3d[0].shape[-2:])

@@ -112,3 +112,41 @@ class TrainLoop:
 
     def state(self) -> Dict[str, np.ndarray]:
         return {k: t.detach().numpy().copy() for k, t in self.params.items()}
+
+
+def reference_epochs(state, fw, train_batches, test_sequences, n_epochs, lr=1e-3, lr_decay=0.95,
+                     causal=False, total_epochs=None):
+    """The epoch loop of run.py:451-558 on CPU: per epoch the training iterations over
+    `train_batches()` (an iterable factory of (batch_cam, batch_3d, batch_2d) numpy
+    batches), the evaluation of the eval-mode model on `test_sequences()` ((cam, 3d, 2d)
+    per sequence), the lr decay and the BatchNorm momentum decay 0.1 -> 0.001
+    (run.py:553-556).  Returns per-epoch (train, valid) losses in metres."""
+    from .temporal_ref import lifter_forward
+    total_epochs = total_epochs or n_epochs
+    loop = TrainLoop(state, fw, causal=causal, lr=lr, amsgrad=True, momentum=0.1)
+    out_train, out_valid = [], []
+    for epoch in range(n_epochs):
+        s = 0.0
+        N = 0
+        for bc, b3, b2 in train_batches():
+            _, loss, _ = loop.step(b2.astype(np.float32), b3.astype(np.float32))
+            n = b3.shape[0] * b3.shape[1]
+            s += n * float(loss)
+            N += n
+        out_train.append(s / N)
+        st = loop.state()
+        s = 0.0
+        N = 0
+        with torch.no_grad():
+            for bc, b3, b2 in test_sequences():
+                y = lifter_forward(st, b2.astype(np.float32), fw, causal=causal)
+                loss = mpjpe(y, torch.from_numpy(b3.astype(np.float32)))
+                n = b3.shape[0] * b3.shape[1]
+                s += n * float(loss)
+                N += n
+        out_valid.append(s / N)
+        for g in loop.opt.param_groups:
+            g["lr"] *= lr_decay
+        e = epoch + 1
+        loop.momentum = 0.1 * np.exp(-e / total_epochs * np.log(0.1 / 0.001))
+    return out_train, out_valid

@@ -11,10 +11,12 @@ Tolerances (f32 on both sides; the native convs accumulate in another order and 
 BN statistics in f64):
   output y           |dy| <= 1e-5 m absolute
   loss               relative 1e-5
-  gradients          per tensor max|g - g64| <= max(2e-4 * max|g64|, 4 * max|g32 - g64|),
-                     where g32 / g64 are the oracle's fp32 / fp64 gradients: the native
-                     result is within a few times the reference's own fp32 error (the BN
-                     weight gradients are sums over every row with heavy cancellation)
+  gradients          per tensor ||g - g64|| <= max(1e-4, 4 ||g32 - g64|| / ||g64||) ||g64||
+                     (g32 / g64: the oracle's fp32 / fp64 gradients) and every element within
+                     2e-3 * max|g64|: an activation whose BN output lies within rounding of 0
+                     can take the other side of the ReLU in the two implementations, which
+                     moves single elements by far more than rounding while the tensor as a
+                     whole agrees to ~1e-5
   running stats      relative 1e-5, absolute 1e-6 (batch means near 0)
   weights after Adam Adam's first steps move each weight by about +-lr * sign(g), so a
                      gradient element within rounding of 0 may flip its step: all weights
@@ -80,10 +82,13 @@ def _oracle(state, x, tgt, meta, p=0.0, masks=None, dtype=torch.float32):
 
 def _grad_close(got, g32, g64, what):
     got, g32, g64 = (np.asarray(a, dtype=np.float64) for a in (got, g32, g64))
-    ref_err = np.abs(g32 - g64).max()
-    tol = max(2e-4 * np.abs(g64).max(), 4 * ref_err, 1e-30)
+    nrm = max(np.linalg.norm(g64), 1e-30)
+    rel = np.linalg.norm(got - g64) / nrm
+    ref_rel = np.linalg.norm(g32 - g64) / nrm
     err = np.abs(got - g64).max()
-    assert err <= tol, f"{what}: max|d| {err:.3e} > tol {tol:.3e} (oracle fp32 error {ref_err:.3e})"
+    print(f"{what}: rel {rel:.2e} (oracle fp32 {ref_rel:.2e}), max|d|/max|g| {err / np.abs(g64).max():.2e}")
+    assert rel <= max(1e-4, 4 * ref_rel), f"{what}: relative error {rel:.3e} (oracle fp32 {ref_rel:.3e})"
+    assert err <= 2e-3 * np.abs(g64).max() + 1e-30, f"{what}: max|d| {err:.3e}"
 
 
 def _weights_close(got, want, lr, what):
