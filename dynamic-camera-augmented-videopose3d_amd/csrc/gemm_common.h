@@ -121,7 +121,8 @@ __device__ __forceinline__ void epi_store(const ConvGemmParams& p, int m, int n,
                                           float sc, float sh) {
     // BatchNorm eval as ATen's CPU kernel evaluates it: x * alpha + beta, two roundings
     v = __fadd_rn(__fmul_rn(v, sc), sh);
-    if (p.relu) v = v > 0.f ? v : 0.f;
+    if (p.relu == 1) v = v > 0.f ? v : 0.f;
+    else if (p.relu == 2) v = v > 0.f ? v : v * 0.01f;  // LeakyReLU (nn.LeakyReLU default slope)
     if (p.R) v += to_f32(((const OT*)p.R)[(int64_t)res_row(p, m) * p.ldr + n]);
     ((OT*)p.Y)[(int64_t)m * p.ldy + n] = from_f32<OT>(v);
 }
@@ -212,7 +213,8 @@ __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     v[e] = __fadd_rn(__fmul_rn(v[e], sc[e]), sh[e]);
-                    if (p.relu) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    if (p.relu == 1) v[e] = v[e] > 0.f ? v[e] : 0.f;
+                    else if (p.relu == 2) v[e] = v[e] > 0.f ? v[e] : v[e] * 0.01f;
                 }
                 if (p.R) {
                     const u32x4(&rq)[RW] = res[pass & 1][q];

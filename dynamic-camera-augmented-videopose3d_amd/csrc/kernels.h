@@ -32,7 +32,7 @@ struct ConvGemmParams {
     int T_out, T_in, stride, dil, Ktap, lda;
     int R_T, R_stride, R_off, ldr;
     int ldy;
-    int relu;
+    int relu;  // 0: none, 1: ReLU, 2: LeakyReLU(0.01) (the 16-bit 256x256 kernels: 0/1 only)
 };
 
 enum class Act { F32 = 0, BF16 = 1, F16 = 2 };
@@ -186,5 +186,25 @@ int wgrad_splits(int64_t M, int N, int K, int64_t max_part_floats);
 hipError_t launch_wgrad(const WgradParams& p, int S, int taps, float* dW, hipStream_t s);
 hipError_t launch_adam(const AdamList& L, const AdamHyper& hp, hipStream_t s);
 hipError_t launch_dropout_mask(uint64_t seed, float p, int layer, int64_t n, uint8_t* out, hipStream_t s);
+
+// ---- trajectory lifters, eval mode (seq_lifter.hip, vp3d_seq.cpp) ----
+struct LstmParams {
+    const float* gin;   // layer-0 gate pre-activations per frame: [frame][4H] (x W_ih^T + b_ih + b_hh)
+    int win_stride;     // frame of (window w, step t) = w * win_stride + t
+    int n_win, W, H, L;
+    const float* wih_t[4];  // layer l >= 1: W_ih^T [H][4H]
+    const float* whh_t[4];  // W_hh^T [H][4H]
+    const float* bias[4];   // layer l >= 1: b_ih + b_hh [4H]
+    const float* out_scale; // BatchNorm (eval) of the last hidden state, folded: h * scale + shift
+    const float* out_shift;
+    float* out;             // [n_win][H]
+};
+hipError_t launch_concat_frames(const float* a, int fa, const float* b, int fb, int64_t rows, float* out,
+                                hipStream_t s);
+hipError_t launch_layernorm_rows(const float* X, int d, int64_t n_rows, int W, int win_stride, const float* pe,
+                                 const float* gamma, const float* beta, float eps, float* out, hipStream_t s);
+hipError_t launch_attention(const float* QKV, int n_win, int W, int d, int heads, int last_only, float* O,
+                            hipStream_t s);
+hipError_t launch_lstm(const LstmParams& p, hipStream_t s);
 
 }  // namespace vp3d

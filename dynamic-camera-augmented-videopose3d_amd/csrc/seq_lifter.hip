@@ -1,0 +1,290 @@
+// Kernels of the fork's other trajectory-conditioned lifters in eval mode
+// (SURVEY.md §8(f) rank 4): CoupledTransformer (reference CamTransformer.py:95-205)
+// and CoupledLSTM (CamLSTM.py:47-129), batched over windows or over the sliding
+// windows of one sequence (sliding_window, CamTransformer.py:72-92).  The Linear
+// layers run on the f32 conv-GEMM (conv_gemm.hip); these are the rest:
+//
+//   concat_frames_kernel    [flat 2D | flat K.E] rows (CamTransformer.py:187-190)
+//   pe_layernorm_kernel     LayerNorm(P[frame(w, t)] + pe[t]) per window row: the input
+//                           projection P is computed once per frame and shared by every
+//                           window that contains the frame (:193-195)
+//   layernorm_kernel        the post-norm LayerNorms of nn.TransformerEncoderLayer
+//   attention_kernel        softmax(q k^T / sqrt(dh)) v per (window, head), K and V of
+//                           the window in LDS, one query per thread (online softmax);
+//                           `last_only`: the last encoder layer only needs the last query
+//                           (CamTransformer.py:201 keeps enc_out[:, -1])
+//   lstm_kernel             the stacked nn.LSTM recurrence (gate order i, f, g, o; zero
+//                           initial state) of a tile of windows, persistent over all time
+//                           steps; layer 0's input projection is precomputed per frame
+//
+// f32 throughout (the reference evaluates these models in f32).
+#include "kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace vp3d {
+namespace {
+
+__device__ __forceinline__ float wave_sum(float v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ void concat_frames_kernel(const float* __restrict__ a, int fa, const float* __restrict__ b, int fb,
+                                     int64_t rows, float* __restrict__ out) {
+    const int w = fa + fb;
+    const int64_t total = rows * w;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / w;
+        const int c = (int)(e - r * w);
+        out[e] = c < fa ? a[r * fa + c] : b[r * fb + (c - fa)];
+    }
+}
+
+// One wave per output row m = (w, t): x = X[w * win_stride + t] (+ pe[t]); LayerNorm
+// over d (biased variance, eps), as ATen: y = (x - mean) * rstd * gamma + beta.
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const float* __restrict__ X, int d, int64_t n_rows,
+                                                             int W, int win_stride, const float* __restrict__ pe,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float eps,
+                                                             float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= n_rows) return;
+    const int64_t w = m / W;
+    const int t = (int)(m - w * W);
+    const float* x = X + (w * win_stride + t) * (int64_t)d;
+    float v[16];  // d <= 1024
+    const int per = (d + 63) / 64;
+    float s = 0.f;
+    for (int i = 0; i < per; ++i) {
+        const int c = lane + 64 * i;
+        float xv = 0.f;
+        if (c < d) {
+            xv = x[c];
+            if (pe) xv = xv + pe[(int64_t)t * d + c];
+        }
+        v[i] = xv;
+        s += xv;
+    }
+    const float mean = wave_sum(s) / (float)d;
+    float q = 0.f;
+    for (int i = 0; i < per; ++i) {
+        const int c = lane + 64 * i;
+        const float dv = c < d ? v[i] - mean : 0.f;
+        q += dv * dv;
+    }
+    const float var = wave_sum(q) / (float)d;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    float* o = out + m * d;
+    for (int i = 0; i < per; ++i) {
+        const int c = lane + 64 * i;
+        if (c < d) o[c] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    }
+}
+
+// Multi-head self-attention of one window and one head; QKV rows of 3d floats
+// ([q | k | v], head h at columns h*DH), output O rows of d floats.
+template <int DH>
+__global__ __launch_bounds__(256) void attention_kernel(const float* __restrict__ QKV, int W, int d, int last_only,
+                                                        float scale, float* __restrict__ O) {
+    extern __shared__ float sm[];
+    float* Ks = sm;            // [W][DH]
+    float* Vs = sm + W * DH;   // [W][DH]
+    const int w = blockIdx.x, h = blockIdx.y;
+    const int64_t row0 = (int64_t)w * W;
+    const int ld = 3 * d;
+    for (int e = threadIdx.x; e < W * DH; e += blockDim.x) {
+        const int j = e / DH, c = e - j * DH;
+        const float* r = QKV + (row0 + j) * ld + h * DH + c;
+        Ks[e] = r[d];
+        Vs[e] = r[2 * d];
+    }
+    __syncthreads();
+    const int t_begin = last_only ? W - 1 : 0;
+    for (int t = t_begin + (int)threadIdx.x; t < W; t += blockDim.x) {
+        float q[DH], o[DH];
+        const float* qr = QKV + (row0 + t) * ld + h * DH;
+#pragma unroll
+        for (int c = 0; c < DH; ++c) {
+            q[c] = qr[c];
+            o[c] = 0.f;
+        }
+        float mx = -INFINITY, l = 0.f;
+        for (int j = 0; j < W; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int c = 0; c < DH; ++c) s = fmaf(q[c], Ks[j * DH + c], s);
+            s = s * scale;
+            if (s > mx) {
+                const float corr = __expf(mx - s);
+                l *= corr;
+#pragma unroll
+                for (int c = 0; c < DH; ++c) o[c] *= corr;
+                mx = s;
+            }
+            const float pj = __expf(s - mx);
+            l += pj;
+#pragma unroll
+            for (int c = 0; c < DH; ++c) o[c] = fmaf(pj, Vs[j * DH + c], o[c]);
+        }
+        const float inv = 1.0f / l;
+        float* orow = O + (last_only ? (int64_t)w : row0 + t) * d + h * DH;
+#pragma unroll
+        for (int c = 0; c < DH; ++c) orow[c] = o[c] * inv;
+    }
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Stacked LSTM over W steps for a tile of NW windows.  Thread (u, half): hidden unit u
+// (0..H-1) of windows [half*NWH, half*NWH + NWH); it owns that unit's four gates and
+// cell state.  Weights are read transposed ([k][4H], coalesced across units); the
+// previous hidden states of the tile live in LDS.
+constexpr int LSTM_NW = 16;
+constexpr int LSTM_MAXL = 4;
+
+template <int H>
+__global__ __launch_bounds__(2 * H) void lstm_kernel(LstmParams p) {
+    constexpr int NWH = LSTM_NW / 2;
+    __shared__ float hs[LSTM_MAXL][2][LSTM_NW][H];  // [layer][buffer][window][unit]
+    const int u = threadIdx.x % H;
+    const int half = threadIdx.x / H;
+    const int w0 = blockIdx.x * LSTM_NW;
+    for (int e = threadIdx.x; e < LSTM_MAXL * 2 * LSTM_NW * H; e += blockDim.x) (&hs[0][0][0][0])[e] = 0.f;
+    float c[LSTM_MAXL][NWH];
+#pragma unroll
+    for (int l = 0; l < LSTM_MAXL; ++l)
+#pragma unroll
+        for (int i = 0; i < NWH; ++i) c[l][i] = 0.f;
+    __syncthreads();
+    const int G = 4 * H;
+    int cur = 0;
+    for (int t = 0; t < p.W; ++t) {
+        for (int l = 0; l < p.L; ++l) {
+            float acc[4][NWH];
+            // layer input: precomputed projection (l = 0) or the new hidden state of layer l-1
+#pragma unroll
+            for (int i = 0; i < NWH; ++i) {
+                const int w = w0 + half * NWH + i;
+                if (l == 0) {
+                    const float* g = p.gin + ((int64_t)(w < p.n_win ? w : 0) * p.win_stride + t) * G;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q][i] = g[q * H + u];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q][i] = p.bias[l][q * H + u];
+                }
+            }
+            if (l > 0) {
+                const float* WT = p.wih_t[l];  // [H][4H]
+                const float* hin = &hs[l - 1][cur ^ 1][half * NWH][0];
+                for (int k = 0; k < H; ++k) {
+                    float wv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) wv[q] = WT[k * G + q * H + u];
+#pragma unroll
+                    for (int i = 0; i < NWH; ++i) {
+                        const float hv = hin[i * H + k];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) acc[q][i] = fmaf(hv, wv[q], acc[q][i]);
+                    }
+                }
+            }
+            {
+                const float* WT = p.whh_t[l];
+                const float* hprev = &hs[l][cur][half * NWH][0];
+                for (int k = 0; k < H; ++k) {
+                    float wv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) wv[q] = WT[k * G + q * H + u];
+#pragma unroll
+                    for (int i = 0; i < NWH; ++i) {
+                        const float hv = hprev[i * H + k];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) acc[q][i] = fmaf(hv, wv[q], acc[q][i]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NWH; ++i) {
+                const float ig = sigm(acc[0][i]), fg = sigm(acc[1][i]);
+                const float gg = tanhf(acc[2][i]), og = sigm(acc[3][i]);
+                float cc = c[0][0];
+#pragma unroll
+                for (int ll = 0; ll < LSTM_MAXL; ++ll)
+                    if (ll == l) cc = c[ll][i];
+                cc = fg * cc + ig * gg;
+#pragma unroll
+                for (int ll = 0; ll < LSTM_MAXL; ++ll)
+                    if (ll == l) c[ll][i] = cc;
+                hs[l][cur ^ 1][half * NWH + i][u] = og * tanhf(cc);
+            }
+            __syncthreads();
+        }
+        cur ^= 1;
+    }
+    // last hidden state of the top layer -> BatchNorm (eval affine) -> out
+#pragma unroll
+    for (int i = 0; i < NWH; ++i) {
+        const int w = w0 + half * NWH + i;
+        if (w < p.n_win) {
+            const float hv = hs[p.L - 1][cur][half * NWH + i][u];
+            p.out[(int64_t)w * H + u] = hv * p.out_scale[u] + p.out_shift[u];
+        }
+    }
+}
+
+inline int grid1(int64_t n, int per = 256) {
+    int64_t g = (n + per - 1) / per;
+    if (g < 1) g = 1;
+    return (int)(g < 65536 ? g : 65536);
+}
+
+}  // namespace
+
+hipError_t launch_concat_frames(const float* a, int fa, const float* b, int fb, int64_t rows, float* out,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(concat_frames_kernel, dim3(grid1(rows * (fa + fb))), dim3(256), 0, s, a, fa, b, fb, rows, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_layernorm_rows(const float* X, int d, int64_t n_rows, int W, int win_stride, const float* pe,
+                                 const float* gamma, const float* beta, float eps, float* out, hipStream_t s) {
+    if (d > 1024) return hipErrorInvalidValue;
+    if (n_rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(layernorm_rows_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, s, X, d, n_rows, W,
+                       win_stride, pe, gamma, beta, eps, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_attention(const float* QKV, int n_win, int W, int d, int heads, int last_only, float* O,
+                            hipStream_t s) {
+    const int dh = d / heads;
+    if (dh * heads != d) return hipErrorInvalidValue;
+    const float scale = 1.0f / sqrtf((float)dh);
+    const size_t smem = (size_t)2 * W * dh * sizeof(float);
+    if (smem > 64 * 1024) return hipErrorInvalidValue;
+    const dim3 grid(n_win, heads);
+    switch (dh) {
+        case 16: hipLaunchKernelGGL(attention_kernel<16>, grid, dim3(256), smem, s, QKV, W, d, last_only, scale, O); break;
+        case 32: hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(256), smem, s, QKV, W, d, last_only, scale, O); break;
+        case 64: hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(256), smem, s, QKV, W, d, last_only, scale, O); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_lstm(const LstmParams& p, hipStream_t s) {
+    if (p.L < 1 || p.L > LSTM_MAXL) return hipErrorInvalidValue;
+    const dim3 grid((p.n_win + LSTM_NW - 1) / LSTM_NW);
+    switch (p.H) {
+        case 64: hipLaunchKernelGGL(lstm_kernel<64>, grid, dim3(128), 0, s, p); break;
+        case 128: hipLaunchKernelGGL(lstm_kernel<128>, grid, dim3(256), 0, s, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace vp3d

@@ -50,6 +50,8 @@ EXPORTS = [
     "vp3d_stream_destroy",
     "vp3d_trainer_create", "vp3d_trainer_destroy", "vp3d_train_forward", "vp3d_train_backward",
     "vp3d_train_dropout_mask", "vp3d_train_layer_rows", "vp3d_adam_step", "vp3d_mpjpe_backward",
+    "vp3d_seq_weight_count", "vp3d_seq_create", "vp3d_seq_destroy", "vp3d_seq_forward",
+    "vp3d_seq_sliding_window",
 ]
 
 
@@ -65,6 +67,29 @@ class vp3d_cfg(ctypes.Structure):
         ("dense", ctypes.c_int32),
         ("variant", ctypes.c_int32),
         ("bn_eps", ctypes.c_float),
+    ]
+
+
+SEQ_TRANSFORMER = 0
+SEQ_LSTM = 1
+SEQ_MAX_HEAD = 8
+
+
+class vp3d_seq_cfg(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("num_joints_in", ctypes.c_int32),
+        ("in_features", ctypes.c_int32),
+        ("num_joints_out", ctypes.c_int32),
+        ("out_features", ctypes.c_int32),
+        ("d_model", ctypes.c_int32),
+        ("num_layers", ctypes.c_int32),
+        ("n_heads", ctypes.c_int32),
+        ("dim_feedforward", ctypes.c_int32),
+        ("n_head_layers", ctypes.c_int32),
+        ("head_layers", ctypes.c_int32 * SEQ_MAX_HEAD),
+        ("max_len", ctypes.c_int32),
+        ("eps", ctypes.c_float),
     ]
 
 
@@ -119,6 +144,11 @@ _SIGNATURES = {
                               ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),
                               ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                               ctypes.c_double, _i64, _int, _vp]),
+    "vp3d_seq_weight_count": (_int, [ctypes.POINTER(vp3d_seq_cfg)]),
+    "vp3d_seq_create": (_int, [ctypes.POINTER(vp3d_seq_cfg), ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]),
+    "vp3d_seq_destroy": (_int, [_vp]),
+    "vp3d_seq_forward": (_int, [_vp, _vp, _vp, _int, _int, _vp, _vp]),
+    "vp3d_seq_sliding_window": (_int, [_vp, _vp, _vp, _int, _int, _vp, _vp]),
     "vp3d_last_error": (ctypes.c_char_p, []),
     "vp3d_abi_version": (_int, []),
 }

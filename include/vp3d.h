@@ -226,6 +226,56 @@ int vp3d_adam_step(int n, float* const* params, const float* const* grads, float
                    double beta1, double beta2, double eps, double weight_decay, int64_t step, int amsgrad,
                    void* stream);
 
+/* ---- trajectory-conditioned sequence lifters, eval mode ----
+ * CoupledTransformer (common/models/CamTransformer.py:95-205) and CoupledLSTM
+ * (common/models/CamLSTM.py:47-129): per frame [flat 2D | flat K.E] (:187-190 /
+ * :115-121), then a transformer encoder or a stacked LSTM over a window, the last
+ * step through an MLP head.  f32. */
+#define VP3D_SEQ_TRANSFORMER 0
+#define VP3D_SEQ_LSTM 1
+#define VP3D_SEQ_MAX_HEAD 8
+
+typedef struct vp3d_seq_cfg {
+    int32_t kind;            /* VP3D_SEQ_*                                                 */
+    int32_t num_joints_in, in_features, num_joints_out, out_features;
+    int32_t d_model;         /* transformer d_model / LSTM hidden_size                     */
+    int32_t num_layers;      /* encoder layers / LSTM cells (<= 4)                         */
+    int32_t n_heads;         /* transformer only; d_model / n_heads in {16, 32, 64}        */
+    int32_t dim_feedforward; /* transformer only                                           */
+    int32_t n_head_layers;   /* len(head_layers)                                           */
+    int32_t head_layers[VP3D_SEQ_MAX_HEAD];
+    int32_t max_len;         /* rows of the positional-encoding table (5000)               */
+    float eps;               /* LayerNorm / BatchNorm eps (1e-5)                           */
+} vp3d_seq_cfg;
+
+typedef struct vp3d_seq_lifter vp3d_seq_lifter;
+
+/* Host weight arrays vp3d_seq_create expects, in state_dict order without the
+ * BatchNorm num_batches_tracked counters:
+ *   transformer: input_projection.{weight, bias}, positional_encoding.pe (max_len x d),
+ *     pre_transformer_norm.{weight, bias}, per encoder layer self_attn.in_proj_{weight, bias},
+ *     self_attn.out_proj.{weight, bias}, linear1.{weight, bias}, linear2.{weight, bias},
+ *     norm1.{weight, bias}, norm2.{weight, bias}; mlp_layers Linear {weight, bias} x (heads + 1)
+ *   lstm: per cell weight_ih, weight_hh, bias_ih, bias_hh; bn_lstm.{weight, bias,
+ *     running_mean, running_var}; per head layer Linear {weight, bias} + BatchNorm1d
+ *     {weight, bias, running_mean, running_var}; the last Linear {weight, bias}
+ * Returns the count, or -1 for an invalid configuration. */
+int vp3d_seq_weight_count(const vp3d_seq_cfg* cfg);
+int vp3d_seq_create(const vp3d_seq_cfg* cfg, const float* const* weights, int n_weights, vp3d_seq_lifter** out);
+int vp3d_seq_destroy(vp3d_seq_lifter* h);
+
+/* forward(input_2d, input_cam) (CamTransformer.py:165-205, CamLSTM.py:104-129):
+ * x2d device f32 (B, T, J_in, F), xcam device f32 (B, T, 3, 4) -> y device f32
+ * (B, 1, J_out, out_features). */
+int vp3d_seq_forward(vp3d_seq_lifter* h, const float* x2d, const float* xcam, int B, int T, float* y, void* stream);
+
+/* sliding_window(inputs_2d, inputs_cam, window) (CamTransformer.py:72-92): x2d (L, J_in, F),
+ * xcam (L, 3, 4) of one sequence -> y (L - window + 1, J_out, out_features), window w =
+ * frames [w, w + window).  The per-frame input projection is shared by all windows; no
+ * (n_windows, window, ...) copy is made. */
+int vp3d_seq_sliding_window(vp3d_seq_lifter* h, const float* x2d, const float* xcam, int L, int window, float* y,
+                            void* stream);
+
 /* ---- on-device input path (common/camera.py, common/generators.py) ---- */
 
 /* normalize_screen_coordinates (camera.py:14-18): out = X/w*2 - [1, h/w] for

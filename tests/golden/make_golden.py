@@ -298,9 +298,54 @@ def train_goldens():
     train_case("train_dense_c32", False, F3, 2, 40, channels=32, dense=True)
 
 
+def seq_lifter_case(name, kind, B=6, L=260, seed=0):
+    """Eval-mode CoupledTransformer / CoupledLSTM (CamTransformer.py:95-205,
+    CamLSTM.py:47-129) at the run.py defaults (arguments.py:41-54): forward on B
+    windows of 243 frames and sliding_window over one padded sequence of L frames
+    (run.py:713).  Weights: torch's default init under manual_seed, BN statistics
+    randomised; stored in the fixture."""
+    from common.models import CamLSTM as ref_lstm
+    from common.models import CamTransformer as ref_tfm
+    torch.manual_seed(seed)
+    if kind == "transformer":
+        m = ref_tfm.CoupledTransformer(17, 2, 17, 3, d_model=128, num_layers=2, n_heads=4, dim_feedforward=128,
+                                       head_layers=[128, 128, 128], dropout=0.25)
+    else:
+        m = ref_lstm.CoupledLSTM(17, 2, 17, 3, hidden_size=128, num_cells=2, head_layers=[128, 128, 128],
+                                 dropout=0.25)
+        for i, bn in enumerate(m.bn_layers):
+            n = bn.num_features
+            bn.running_mean.copy_(torch.from_numpy(synth.uniform(seed + i, name + "/mu", (n,), -0.2, 0.2).astype(np.float32)))
+            bn.running_var.copy_(torch.from_numpy(synth.uniform(seed + i, name + "/var", (n,), 0.5, 2.0).astype(np.float32)))
+            bn.weight.data.copy_(torch.from_numpy(synth.uniform(seed + i, name + "/g", (n,), 0.5, 1.5).astype(np.float32)))
+            bn.bias.data.copy_(torch.from_numpy(synth.uniform(seed + i, name + "/b", (n,), -0.1, 0.1).astype(np.float32)))
+    m.eval()
+    x2 = synth.normalized_windows(seed + 1, name, B, 243)
+    xc = (synth.normal(seed + 2, name + "/cam", (B, 243, 3, 4), std=0.5)).astype(np.float32)
+    s2 = synth.normalized_windows(seed + 3, name + "/seq", 1, L)
+    sc = (synth.normal(seed + 4, name + "/seqcam", (1, L, 3, 4), std=0.5)).astype(np.float32)
+    with torch.no_grad():
+        y = m(torch.from_numpy(x2), torch.from_numpy(xc)).numpy()
+        ys = m.sliding_window(torch.from_numpy(s2), torch.from_numpy(sc), 243).numpy()
+    arrays = {"x2d": x2, "xcam": xc, "y": y, "seq2d": s2, "seqcam": sc, "yseq": ys}
+    for k, v in m.state_dict().items():
+        if not k.endswith(".pe"):  # the sinusoid table (5000 x d) is recomputed, not stored
+            arrays["w/" + k] = v.numpy()
+    meta = dict(kind=kind, B=B, L=L, window=243, seed=seed, keys=list(m.state_dict().keys()),
+                d_model=128, num_layers=2, n_heads=4, dim_feedforward=128, hidden_size=128, num_cells=2,
+                head_layers=[128, 128, 128])
+    arrays["meta"] = np.array(json.dumps(meta))
+    save(name, **arrays)
+
+
+def seq_lifter_goldens():
+    seq_lifter_case("cam_transformer", "transformer")
+    seq_lifter_case("cam_lstm", "lstm")
+
+
 GROUPS = {"run_eval": run_eval_golden, "model": model_goldens, "generator": generator_goldens,
           "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens,
-          "train": train_goldens}
+          "train": train_goldens, "seq_lifter": seq_lifter_goldens}
 
 if __name__ == "__main__":
     # python make_golden.py [group ...]  (default: every group); the manifest is merged
