@@ -56,12 +56,15 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="training iteration (f32): TemporalModel train mode + backward + Adam; "
                          "--batch defaults to 1024 windows (run.py's batch_size)")
+    ap.add_argument("--seq-model", choices=["transformer", "lstm"], default=None,
+                    help="sliding-window eval of CoupledTransformer / CoupledLSTM (f32); --batch = poses "
+                         "per step (default 16384)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="approximate CPU-baseline sample duration (0 disables)")
     ap.add_argument("--parity-windows", type=int, default=32)
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = 1024 if args.train else 8192
+        args.batch = 1024 if args.train else (16384 if args.seq_model else 8192)
     return args
 
 
@@ -301,6 +304,108 @@ def train_cpu_baseline(sd, RF, seconds):
                       f"(oracle/train_ref.py: torch-CPU autograd + Adam) in {dt:.1f} s"}
 
 
+def seq_flop_per_pose(kind, W=243, d=128, layers=2, ff=128, heads=4, head=(128, 128, 128), cin=46, jout=51,
+                      shared_projection=True):
+    """Algorithmic FLOP of one sliding-window pose of CoupledTransformer / CoupledLSTM at the
+    run.py defaults, as the native path evaluates it: the per-frame input projection once per
+    frame (shared by the W windows that contain it), the last encoder layer for the last
+    query only (the model keeps enc_out[:, -1]); softmax/LayerNorm/activations excluded."""
+    if kind == "transformer":
+        f = 2 * cin * d  # input projection, one new frame per window
+        for l in range(layers):
+            last = l == layers - 1
+            f += 2 * W * d * 3 * d                                   # q, k, v projections
+            q = 1 if last else W
+            f += 2 * 2 * q * W * d                                   # q k^T and p v
+            f += 2 * q * d * d + 2 * 2 * q * d * ff                  # out proj, feed-forward
+    else:
+        H = d
+        f = 2 * cin * 4 * H
+        f += W * 2 * (4 * H * H)                                     # layer-0 recurrence
+        f += (layers - 1) * W * 2 * (2 * 4 * H * H)                  # upper cells: input + recurrence
+    w = d
+    for h in head:
+        f += 2 * w * h
+        w = h
+    f += 2 * w * jout
+    return f
+
+
+def seq_main(args, world, rank, dev):
+    """Sliding-window evaluation of the trajectory lifters: one step
+    = model.sliding_window over one padded sequence of N + 242 frames -> N poses
+    (run.py:713), CoupledTransformer / CoupledLSTM at the run.py defaults, f32."""
+    from vp3d_amd import synth
+    kind = args.seq_model
+    torch.manual_seed(0)
+    if kind == "transformer":
+        from common.models.CamTransformer import CoupledTransformer
+        model = CoupledTransformer(JOINTS, 2, JOINTS, 3, 128, 2, 4, 128, [128, 128, 128])
+    else:
+        from common.models.CamLSTM import CoupledLSTM
+        model = CoupledLSTM(JOINTS, 2, JOINTS, 3, 128, 2, [128, 128, 128])
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    model.cuda().eval()
+    W = 243
+    N = args.batch
+    L = N + W - 1
+    x2 = synth_windows(1, L, JOINTS, 1000 + rank, dev)
+    xc = (torch.randn((1, L, 3, 4), device=dev) * 0.5).contiguous()
+    lifter = model.native_lifter(dev)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            y = lifter.sliding_window(x2, xc, W)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            y = lifter.sliding_window(x2, xc, W)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        return
+    flop = seq_flop_per_pose(kind)
+    poses_s = world * N * args.steps / dt
+    out = {
+        "metric": f"3D poses/sec, {'CoupledTransformer' if kind == 'transformer' else 'CoupledLSTM'} sliding window "
+                  "(243-frame window, 17 joints, camera-trajectory input)",
+        "value": round(poses_s, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded sequence, torch-default-init weights)",
+        "config": {"workload": f"sliding_window of {kind} over {L} frames (run.py:713)", "poses_per_step": N,
+                   "parallelism": f"dp{world} (independent sequences)"},
+        "flop_per_pose": flop, "tflops_effective": round(poses_s * flop / 1e12, 3),
+    }
+    if args.cpu_seconds > 0:
+        from oracle.seq_lifter_ref import lstm_forward, sliding_windows, transformer_forward
+        threads = torch.get_num_threads()
+        n = 0
+        x2c, xcc = x2.cpu(), xc.cpu()
+        t0 = time.perf_counter()
+        pos = 0
+        while time.perf_counter() - t0 < args.cpu_seconds and pos + 64 <= N:
+            w2, wc = sliding_windows(x2c[:, pos:pos + 64 + W - 1], xcc[:, pos:pos + 64 + W - 1], W)
+            if kind == "transformer":
+                transformer_forward(sd, w2, wc, 4, 2, 3)
+            else:
+                lstm_forward(sd, w2, wc, 128, 2, 3)
+            n += 64
+            pos += 64
+        dtc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n / dtc, 2), "unit": "poses/s", "cores": threads, "kind": "port",
+                               "sample": f"{n} sliding windows (batches of 64) through oracle/seq_lifter_ref.py "
+                                         f"(torch-CPU, the reference's op sequence) in {dtc:.1f} s"}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,8 +415,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if args.stream or args.train:
-        (train_main if args.train else stream_main)(args, world, rank, dev)
+    if args.stream or args.train or args.seq_model:
+        (train_main if args.train else seq_main if args.seq_model else stream_main)(args, world, rank, dev)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
