@@ -221,25 +221,18 @@ def train_main(args, world, rank, dev):
     B = args.batch
     x = synth_windows(B, RF, JOINTS, 1000 + rank, dev)
     tgt = (torch.randn((B, 1, JOINTS, 3), device=dev) * 0.2).contiguous()
+    from common.loss import mpjpe
+    from vp3d_amd.shard import allreduce_gradients
     params = [p for p in model.parameters()]
-    flat = None
-    if world > 1:
-        flat = torch.empty(sum(p.numel() for p in params), device=dev)
+    bucket = [None]
 
     def step():
         y = model(x)
-        loss = torch.mean(torch.norm(y - tgt, dim=-1))
+        loss = mpjpe(y, tgt)
         opt.zero_grad(set_to_none=False)
         loss.backward()
-        if world > 1:
-            # one bucket: every gradient in one RCCL all_reduce (68 MB)
-            torch.cat([p.grad.reshape(-1) for p in params], out=flat)
-            dist.all_reduce(flat)
-            flat.div_(world)
-            o = 0
-            for p in params:
-                p.grad.copy_(flat[o:o + p.numel()].view_as(p))
-                o += p.numel()
+        # data parallel: one all_reduce of one flat gradient bucket (68 MB, RCCL)
+        bucket[0] = allreduce_gradients(params, bucket[0])
         opt.step()
         return loss
 

@@ -76,3 +76,33 @@ def test_gloo_world2(tmp_path):
     want = float(np.mean(np.linalg.norm(y_full.astype(np.float64) - gt, axis=-1)))
     for p in parts:
         assert abs(float(p["g"]) - want) < 1e-6
+
+
+def _grad_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(100 + rank)
+    params = [torch.nn.Parameter(torch.zeros(s)) for s in [(7, 3), (11,), (2, 5, 4)]]
+    for p in params:
+        p.grad = torch.randn(p.shape)
+    mine = [p.grad.clone() for p in params]
+    flat = shard.allreduce_gradients(params)
+    flat2 = shard.allreduce_gradients(params, flat)  # reuses the bucket
+    assert flat2 is flat
+    np.savez(os.path.join(outdir, f"g{rank}.npz"), *[m.numpy() for m in mine],
+             *[p.grad.numpy() for p in params])
+    dist.destroy_process_group()
+
+
+def test_allreduce_gradients_gloo_world2(tmp_path):
+    """Data-parallel training's gradient averaging (one flat-bucket all_reduce per step):
+    after two calls every rank holds the mean of the ranks' gradients (the second call
+    averages identical values, so it is idempotent)."""
+    port = _free_port()
+    mp.spawn(_grad_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    g = [np.load(os.path.join(tmp_path, f"g{r}.npz")) for r in range(2)]
+    for i in range(3):
+        want = (g[0][f"arr_{i}"] + g[1][f"arr_{i}"]) / 2
+        for r in range(2):
+            np.testing.assert_allclose(g[r][f"arr_{i + 3}"], want, rtol=1e-6, atol=1e-7)
