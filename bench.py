@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--train", action="store_true",
                     help="training iteration (f32): TemporalModel train mode + backward + Adam; "
                          "--batch defaults to 1024 windows (run.py's batch_size)")
+    ap.add_argument("--sequence", action="store_true",
+                    help="sequence mode: dilated TemporalModel over one long sequence (run.py --evaluate "
+                         "shape); --batch = output poses per step (default 65536)")
     ap.add_argument("--seq-model", choices=["transformer", "lstm"], default=None,
                     help="sliding-window eval of CoupledTransformer / CoupledLSTM (f32); --batch = poses "
                          "per step (default 16384)")
@@ -64,7 +67,7 @@ def parse():
     ap.add_argument("--parity-windows", type=int, default=32)
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = 1024 if args.train else (16384 if args.seq_model else 8192)
+        args.batch = 1024 if args.train else (16384 if args.seq_model else 65536 if args.sequence else 8192)
     return args
 
 
@@ -399,6 +402,91 @@ def seq_main(args, world, rank, dev):
     print(json.dumps(out), flush=True)
 
 
+def sequence_main(args, world, rank, dev):
+    """Sequence mode (SURVEY.md §8(d) "also report"): the dilated TemporalModel over one
+    long edge-padded sequence, the run.py --evaluate shape (UnchunkedGenerator, B = 1,
+    T_out + 242 frames in, T_out poses out); bf16 by default.  FLOP(T_out) =
+    2 * (16,933,888 * T_out + 2,591,981,568)."""
+    from common.models.TemporalModel import TemporalModel
+    from oracle.temporal_ref import lifter_forward
+    from vp3d_amd import synth
+
+    model = TemporalModel(JOINTS, 2, JOINTS, FW, channels=CHANNELS)
+    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.eval().cuda().set_compute_dtype(args.dtype)
+    RF = model.receptive_field()
+    T_out = args.batch
+    x = synth_windows(1, T_out + RF - 1, JOINTS, 1000 + rank, dev)
+    lifter = model.native_lifter(dev)
+    lifter.reserve(1, T_out + RF - 1, args.dtype)
+    y = torch.empty((1, T_out, JOINTS, 3), device=dev)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            lifter.forward(x, args.dtype, out=y)
+        torch.cuda.synchronize()
+        lifter.profile(True)
+        lifter.profile_reset()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            lifter.forward(x, args.dtype, out=y)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        lifter.profile(False)
+    prof = lifter.profile_read()
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        return
+    value = world * T_out * args.steps / dt
+    flop_step = 2 * (16933888 * T_out + 2591981568)
+    dom = max(prof, key=lambda r: r["ms_total"])
+    dom_ms = dom["ms_total"] / max(dom["launches"], 1)
+    names = ["expand"] + [f"block{(i // 2) + 1}_{'k3' if i % 2 == 0 else '1x1'}"
+                          for i in range(2 * (len(FW) - 1))] + ["shrink"]
+    # parity on the first 256 output frames (a time shard: inputs [0, 256 + RF - 1))
+    P = min(256, T_out)
+    ref = lifter_forward(sd, x[:, :P + RF - 1].cpu(), FW).numpy()
+    got = y[:, :P].cpu().numpy()
+    out = {
+        "metric": "3D poses/sec, dilated TemporalModel sequence mode (243-frame RF, 17 joints, 1024ch)",
+        "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded random-walk sequence, counter-hash weights)",
+        "config": {"workload": f"TemporalModel (dilated) on one sequence of {T_out + RF - 1} frames -> {T_out} poses "
+                               "(run.py --evaluate, UnchunkedGenerator)", "poses_per_step": T_out,
+                   "parallelism": f"dp{world} (independent sequences)"},
+        "flop_per_step": flop_step, "tflops_effective": round(value / T_out * flop_step / 1e12, 2),
+        "roofline": {"bound": "mfma", "kernel": f"conv_gemm ({names[dom['layer']]})",
+                     "achieved": round(dom["flop"] / (dom_ms * 1e-3) / 1e12, 2), "peak": PEAK_TFLOPS[args.dtype],
+                     "unit": "TFLOP/s", "frac": round(dom["flop"] / (dom_ms * 1e-3) / 1e12 / PEAK_TFLOPS[args.dtype], 4),
+                     "traffic": None, "avg_launch_ms": round(dom_ms, 4), "flop_per_launch": dom["flop"]},
+        "per_layer_ms": {names[r["layer"]]: round(r["ms_total"] / max(r["launches"], 1), 4) for r in prof},
+        "parity": {"frames_checked": P, "max_coord_delta_mm": float(np.abs(got - ref).max()) * 1e3},
+    }
+    if args.cpu_seconds > 0:
+        nthr = torch.get_num_threads()
+        Tc = 2048
+        xc = x[:, :Tc + RF - 1].cpu()
+        n, t_cpu = 0, 0.0
+        while t_cpu < args.cpu_seconds:
+            t1 = time.perf_counter()
+            lifter_forward(sd, xc, FW)
+            t_cpu += time.perf_counter() - t1
+            n += Tc
+        out["cpu_baseline"] = {"value": round(n / t_cpu, 2), "unit": "poses/s", "cores": nthr, "kind": "port",
+                               "sample": f"{n} poses as sequences of {Tc + RF - 1} frames through oracle/temporal_ref.py "
+                                         f"(torch-CPU, fp32) in {t_cpu:.1f} s"}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -408,8 +496,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if args.stream or args.train or args.seq_model:
-        (train_main if args.train else seq_main if args.seq_model else stream_main)(args, world, rank, dev)
+    if args.stream or args.train or args.seq_model or args.sequence:
+        fn = (train_main if args.train else seq_main if args.seq_model else
+              sequence_main if args.sequence else stream_main)
+        fn(args, world, rank, dev)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()

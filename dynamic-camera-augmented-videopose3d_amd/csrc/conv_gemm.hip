@@ -316,8 +316,8 @@ hipError_t launch_f32(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t
 }
 
 // Which 256x256 kernel a large layer runs on (VP3D_GEMM overrides for A/B runs):
-//   default: the ping-pong kernel (conv_gemm_8p.hip) for layers without a residual
-//   (the k-tap convs: 1.20 vs 1.22 ms on block 1 at B = 8192), the LDS-ring kernel
+//   default: the ping-pong kernel (conv_gemm_8p.hip) for contiguous-tap layers without a
+//   residual (the strided k-tap convs: 1.20 vs 1.22 ms on block 1 at B = 8192), the LDS-ring kernel
 //   (conv_gemm_big.hip) for the 1x1 convs with a residual (0.56 vs 0.58 ms);
 //   VP3D_GEMM=8p -> 8p everywhere; big / persist / pp / tp -> that schedule everywhere.
 int gemm_8p_mode() {
@@ -330,10 +330,87 @@ int gemm_8p_mode() {
 }
 bool gemm_8p_env(const ConvGemmParams& p) {
     const int m = gemm_8p_mode();
-    return m == 2 || (m == 1 && p.R == nullptr);
+    // default: the ping-pong kernel for contiguous-tap convs without a residual (the
+    // strided k3 convs of Optimized1f); the dilated k3 convs (taps gathered from rows d
+    // apart) run faster on the LDS-ring kernel (sequence mode, 65,536 frames: 0.39-0.40 vs
+    // 0.42 ms per layer)
+    return m == 2 || (m == 1 && p.R == nullptr && p.dil == 1);
 }
 
 bool aligned(const void* ptr, uintptr_t a) { return (reinterpret_cast<uintptr_t>(ptr) & (a - 1)) == 0; }
+
+
+// ---------------------------------------------------------------------------
+// narrow layers (N <= 64: the shrink conv, TemporalModel.py:33 / :74) on the 16-bit
+// path: one workgroup per 16 rows x 64 output channels, K streamed straight from global
+// memory into MFMA fragments (the 16-bit weights, <= 128 KiB, stay in L2), f32 out.
+// The 128x128 tile would give the whole layer only M/128 workgroups.
+// ---------------------------------------------------------------------------
+template <typename CT>
+__global__ __launch_bounds__(256) void conv_gemm_narrow(ConvGemmParams p) {
+    // 4 waves split K four ways (short dependent load->MFMA chains), partial 16x64
+    // tiles summed through LDS by wave 0
+    __shared__ float red[3][16][65];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int m0 = blockIdx.x * 16;
+    const int r = lane & 15, kc = (lane >> 4) * 8;
+    const int m = m0 + r;
+    const bool mv = m < p.M;
+    const CT* arow = (const CT*)p.A + (int64_t)(mv ? src_row(p, m) : 0) * p.lda;
+    const CT* W = (const CT*)p.W;
+    const int ksteps = p.K / 32;
+    const int kb = (ksteps * wid) / 4, ke = (ksteps * (wid + 1)) / 4;
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = kb; ks < ke; ks += 2) {
+        const bool two = ks + 1 < ke;
+        const int k0 = ks * 32;
+        u32x4 a0 = mv ? *(const u32x4*)(arow + k0 + kc) : u32x4{0, 0, 0, 0};
+        u32x4 a1 = (mv && two) ? *(const u32x4*)(arow + k0 + 32 + kc) : u32x4{0, 0, 0, 0};
+        u32x4 b0[4], b1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            b0[j] = *(const u32x4*)(W + (int64_t)(j * 16 + r) * p.Kp + k0 + kc);
+            b1[j] = two ? *(const u32x4*)(W + (int64_t)(j * 16 + r) * p.Kp + k0 + 32 + kc) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = mfma16<CT>(a0, b0[j], acc[j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = mfma16<CT>(a1, b1[j], acc[j]);
+    }
+    // D[i = 4*(lane/16) + q][n = j*16 + lane%16]
+    if (wid > 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[wid - 1][(lane >> 4) * 4 + q][j * 16 + r] = acc[j][q];
+    }
+    __syncthreads();
+    if (wid != 0) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = j * 16 + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = (lane >> 4) * 4 + q;
+            float v = acc[j][q];
+            v = v + red[0][i][n];
+            v = v + red[1][i][n];
+            v = v + red[2][i][n];
+            const int mm = m0 + i;
+            if (n < p.N && mm < p.M) epi_store<float>(p, mm, n, v, p.scale[n], p.shift[n]);
+        }
+    }
+}
+
+bool narrow_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
+    // only while the 128-row tiles would leave CUs idle (< 256 tiles): B = 8192 windows
+    // 0.036 -> 0.018 ms; at 65,536 rows the tile kernel stays ahead (0.048 vs 0.086 ms)
+    return compute != Act::F32 && a_type == compute && out_type == Act::F32 && p.N <= 64 && p.M < 256 * BM &&
+           p.Ktap == p.K &&
+           p.K % 32 == 0 && p.Kp >= 64 && p.lda % 8 == 0 && aligned(p.A, 16) && !p.R;
+}
 
 }  // namespace
 
@@ -357,6 +434,14 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     }
     if (a_type != Act::F32 && a_type != compute) return hipErrorInvalidValue;
     if (out_type != Act::F32 && out_type != compute) return hipErrorInvalidValue;
+    if (narrow_eligible(p, a_type, out_type, compute)) {
+        const dim3 g((p.M + 15) / 16);
+        if (compute == Act::BF16)
+            hipLaunchKernelGGL(conv_gemm_narrow<bf16>, g, dim3(256), 0, stream, p);
+        else
+            hipLaunchKernelGGL(conv_gemm_narrow<f16>, g, dim3(256), 0, stream, p);
+        return hipGetLastError();
+    }
     if (conv_gemm_tp_eligible(p, a_type, out_type, compute)) return launch_conv_gemm_tp(p, compute, stream);
     if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_8p_eligible(p, a_type, out_type, compute))
