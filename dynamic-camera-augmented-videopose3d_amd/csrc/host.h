@@ -85,6 +85,7 @@ struct vp3d_handle {
     size_t gather_bytes = 0;
     // profiling
     bool profiling = false;
+    uint64_t prof_mask = ~0ull;  // layers timed while profiling (bit i = layer i)
     std::vector<vp3d::host::ProfEvent> pending;
     std::vector<hipEvent_t> free_events;
     std::vector<double> prof_ms;

@@ -490,7 +490,8 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         }
         // algorithmic FLOP of the layer (unpadded K), timed from before any packing
         ProfEvent pe{};
-        if (h->profiling) {
+        const bool timed = h->profiling && li < 64 && ((h->prof_mask >> li) & 1);
+        if (timed) {
             pe.layer = li;
             pe.a = get_event(h);
             pe.b = get_event(h);
@@ -546,7 +547,7 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         if (e != hipSuccess)
             return fail(VP3D_ERR_HIP, std::string("conv layer ") + std::to_string(li) + ": " +
                                           hipGetErrorString(e));
-        if (h->profiling) {
+        if (timed) {
             hipEventRecord(pe.b, s);
             h->pending.push_back(pe);
         }
@@ -595,6 +596,12 @@ int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const flo
 int vp3d_profile_enable(vp3d_handle* h, int enable) {
     if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
     h->profiling = enable != 0;
+    return VP3D_OK;
+}
+
+int vp3d_profile_layers(vp3d_handle* h, uint64_t mask) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    h->prof_mask = mask;
     return VP3D_OK;
 }
 

@@ -142,6 +142,11 @@ class NativeLifter:
     def profile(self, enable: bool) -> None:
         N.check(self._lib.vp3d_profile_enable(self._h, 1 if enable else 0))
 
+    def profile_layers(self, layers=None) -> None:
+        """Time only `layers` (indices; None = all) while profiling is enabled."""
+        mask = (1 << 64) - 1 if layers is None else sum(1 << int(i) for i in layers)
+        N.check(self._lib.vp3d_profile_layers(self._h, mask))
+
     def profile_reset(self) -> None:
         with torch.cuda.device(self.device):
             N.check(self._lib.vp3d_profile_reset(self._h))

@@ -130,6 +130,9 @@ int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const flo
 
 /* ---- per-layer timing (HIP events recorded on the launch stream) ---- */
 int vp3d_profile_enable(vp3d_handle* h, int enable);
+/* Restrict the timing to the layers in `mask` (bit i = layer i; all by default), e.g.
+ * only the dominant layer inside a timed loop so the other launches carry no events. */
+int vp3d_profile_layers(vp3d_handle* h, uint64_t mask);
 /* Number of kernel launches one forward makes (conv layers incl. shrink). */
 int vp3d_layer_count(const vp3d_handle* h);
 /* Accumulated time (ms) and launch count per layer since the last reset, and
