@@ -136,6 +136,171 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* __restrict_
     }
 }
 
+// Full self-attention of one (window, head) on the f32 MFMA (v_mfma_f32_16x16x4_f32):
+// each wave takes 16-query tiles; S^T = K Q^T per 16-key block (keys down the
+// accumulator rows, queries across lanes), softmax over the keys in registers plus two
+// cross-lane-group shuffles, then O^T += V^T P^T where P^T is consumed straight from the
+// S^T accumulators (the MFMA k-slot of lane group g, register r is key 4g + r of the
+// block on both operands, so no transpose is needed).  K and V in LDS, row pitch 36
+// floats (conflict-free for both access patterns).
+constexpr int ATT_LD = 36;
+constexpr int ATT_WMAX = 256;
+
+template <int DH>
+__global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __restrict__ QKV, int W, int d,
+                                                             float scale, float* __restrict__ O) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    static_assert(DH == 16 || DH == 32, "head dim");
+    __shared__ float Ks[ATT_WMAX * ATT_LD];
+    __shared__ float Vs[ATT_WMAX * ATT_LD];
+    const int w = blockIdx.x, h = blockIdx.y;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t row0 = (int64_t)w * W;
+    const int ld = 3 * d;
+    const int nkb = (W + 15) / 16;
+    for (int e = threadIdx.x; e < nkb * 16 * DH; e += blockDim.x) {
+        const int j = e / DH, c = e - j * DH;
+        float kv = 0.f, vv = 0.f;
+        if (j < W) {
+            const float* r = QKV + (row0 + j) * ld + h * DH + c;
+            kv = r[d];
+            vv = r[2 * d];
+        }
+        Ks[j * ATT_LD + c] = kv;
+        Vs[j * ATT_LD + c] = vv;
+    }
+    __syncthreads();
+    const int g = lane >> 4, lq = lane & 15;
+    constexpr int NS = DH / 4;
+    for (int qt = wid; qt < nkb; qt += 4) {
+        const int q = qt * 16 + lq;
+        float qf[NS];
+        const float* qr = QKV + (row0 + (q < W ? q : W - 1)) * ld + h * DH;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) qf[s] = qr[4 * s + g] * scale;
+        f32x4 S[ATT_WMAX / 16];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < ATT_WMAX / 16; ++kb) {
+            if (kb < nkb) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                const float* kr = Ks + (kb * 16 + lq) * ATT_LD + g;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[4 * s], qf[s], acc, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (kb * 16 + 4 * g + r >= W) acc[r] = -INFINITY;
+                    mx = fmaxf(mx, acc[r]);
+                }
+                S[kb] = acc;
+            }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float l = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < ATT_WMAX / 16; ++kb) {
+            if (kb < nkb) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float p = __expf(S[kb][r] - mx);
+                    S[kb][r] = p;
+                    l += p;
+                }
+            }
+        }
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        f32x4 o[DH / 16];
+#pragma unroll
+        for (int ib = 0; ib < DH / 16; ++ib) o[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < ATT_WMAX / 16; ++kb) {
+            if (kb < nkb) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float* vr = Vs + (kb * 16 + 4 * g + r) * ATT_LD + lq;
+#pragma unroll
+                    for (int ib = 0; ib < DH / 16; ++ib)
+                        o[ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[ib * 16], S[kb][r], o[ib], 0, 0, 0);
+                }
+            }
+        }
+        // o[ib][r]: dim ib*16 + 4g + r of query qt*16 + lq
+        if (q < W) {
+            const float inv = 1.0f / l;
+            float* orow = O + (row0 + q) * d + h * DH;
+#pragma unroll
+            for (int ib = 0; ib < DH / 16; ++ib) {
+                f32x4 v = o[ib];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = v[r] * inv;
+                *(f32x4*)(orow + ib * 16 + 4 * g) = v;
+            }
+        }
+    }
+}
+
+// Attention of the LAST query only (the last encoder layer: CamTransformer.py:201 keeps
+// enc_out[:, -1]): one wave per (window, head), lanes over the keys; each lane streams its
+// keys' K and V rows (DH contiguous floats) once, softmax by wave reductions, the 64
+// per-lane partial outputs summed through LDS.  Bandwidth-bound on the K/V rows.
+template <int DH>
+__global__ __launch_bounds__(1024) void attention_last_kernel(const float* __restrict__ QKV, int W, int d,
+                                                              float scale, float* __restrict__ O) {
+    __shared__ float part[16][64][DH + 1];
+    const int w = blockIdx.x;
+    const int h = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row0 = (int64_t)w * W;
+    const int ld = 3 * d;
+    float q[DH];
+    const float* qr = QKV + (row0 + W - 1) * ld + h * DH;
+#pragma unroll
+    for (int c = 0; c < DH; ++c) q[c] = qr[c] * scale;
+    constexpr int KPL = 4;  // keys per lane (W <= 256)
+    float sc[KPL];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+        const int j = lane + 64 * i;
+        float sv = -INFINITY;
+        if (j < W) {
+            const float* kr = QKV + (row0 + j) * ld + d + h * DH;
+            float a = 0.f;
+#pragma unroll
+            for (int c = 0; c < DH; ++c) a = fmaf(q[c], kr[c], a);
+            sv = a;
+        }
+        sc[i] = sv;
+        mx = fmaxf(mx, sv);
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float l = 0.f;
+    float acc[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+        const int j = lane + 64 * i;
+        if (j < W) {
+            const float p = __expf(sc[i] - mx);
+            l += p;
+            const float* vr = QKV + (row0 + j) * ld + 2 * d + h * DH;
+#pragma unroll
+            for (int c = 0; c < DH; ++c) acc[c] = fmaf(p, vr[c], acc[c]);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o, 64);
+#pragma unroll
+    for (int c = 0; c < DH; ++c) part[h][lane][c] = acc[c];
+    __syncthreads();
+    if (lane < DH) {
+        float sum = 0.f;
+        for (int i = 0; i < 64; ++i) sum += part[h][i][lane];
+        O[(int64_t)w * d + h * DH + lane] = sum / l;
+    }
+}
+
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Stacked LSTM over W steps for a tile of NW windows.  Thread (u, half): hidden unit u
@@ -267,6 +432,20 @@ hipError_t launch_attention(const float* QKV, int n_win, int W, int d, int heads
     const size_t smem = (size_t)2 * W * dh * sizeof(float);
     if (smem > 64 * 1024) return hipErrorInvalidValue;
     const dim3 grid(n_win, heads);
+    if (last_only && W <= 256 && heads <= 16 && (dh == 16 || dh == 32)) {
+        if (dh == 16)
+            hipLaunchKernelGGL(attention_last_kernel<16>, dim3(n_win), dim3(64 * heads), 0, s, QKV, W, d, scale, O);
+        else
+            hipLaunchKernelGGL(attention_last_kernel<32>, dim3(n_win), dim3(64 * heads), 0, s, QKV, W, d, scale, O);
+        return hipGetLastError();
+    }
+    if (!last_only && W <= ATT_WMAX && (dh == 16 || dh == 32)) {
+        if (dh == 16)
+            hipLaunchKernelGGL(attention_mfma_kernel<16>, grid, dim3(256), 0, s, QKV, W, d, scale, O);
+        else
+            hipLaunchKernelGGL(attention_mfma_kernel<32>, grid, dim3(256), 0, s, QKV, W, d, scale, O);
+        return hipGetLastError();
+    }
     switch (dh) {
         case 16: hipLaunchKernelGGL(attention_kernel<16>, grid, dim3(256), smem, s, QKV, W, d, last_only, scale, O); break;
         case 32: hipLaunchKernelGGL(attention_kernel<32>, grid, dim3(256), smem, s, QKV, W, d, last_only, scale, O); break;
