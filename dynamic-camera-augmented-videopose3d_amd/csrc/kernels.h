@@ -186,6 +186,8 @@ int wgrad_splits(int64_t M, int N, int K, int64_t max_part_floats);
 hipError_t launch_wgrad(const WgradParams& p, int S, int taps, float* dW, hipStream_t s);
 hipError_t launch_adam(const AdamList& L, const AdamHyper& hp, hipStream_t s);
 hipError_t launch_dropout_mask(uint64_t seed, float p, int layer, int64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_relu_mask(const float* Z, int64_t n, int C, const float* alpha, const float* shift, uint8_t* out,
+                            hipStream_t s);
 
 // ---- trajectory lifters, eval mode (seq_lifter.hip, vp3d_seq.cpp) ----
 struct LstmParams {

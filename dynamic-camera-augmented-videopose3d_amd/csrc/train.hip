@@ -473,6 +473,14 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamList L, AdamHyper hp) {
     }
 }
 
+__global__ void relu_mask_kernel(const float* __restrict__ Z, int64_t n, int C, const float* __restrict__ alpha,
+                                 const float* __restrict__ shift, uint8_t* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        out[i] = (Z[i] * alpha[c] + shift[c]) > 0.f ? 1 : 0;
+    }
+}
+
 __global__ void dropout_mask_kernel(uint64_t seed, uint64_t thresh, int layer, int64_t n, uint8_t* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         out[i] = thresh == (1ull << 32) ? 1 : (drop_keep(seed, layer, i, thresh) ? 1 : 0);
@@ -609,6 +617,12 @@ hipError_t launch_wgrad(const WgradParams& p0, int S, int taps, float* dW, hipSt
 hipError_t launch_adam(const AdamList& L, const AdamHyper& hp, hipStream_t s) {
     if (L.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(adam_kernel, dim3(L.block_start[L.n]), dim3(256), 0, s, L, hp);
+    return hipGetLastError();
+}
+
+hipError_t launch_relu_mask(const float* Z, int64_t n, int C, const float* alpha, const float* shift, uint8_t* out,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(n)), dim3(256), 0, s, Z, n, C, alpha, shift, out);
     return hipGetLastError();
 }
 

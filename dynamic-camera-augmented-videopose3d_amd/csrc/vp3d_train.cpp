@@ -449,6 +449,17 @@ int vp3d_train_dropout_mask(vp3d_trainer* t, int layer, int64_t n_elems, uint8_t
     return VP3D_OK;
 }
 
+int vp3d_train_relu_mask(vp3d_trainer* t, int layer, int64_t n_elems, uint8_t* out, void* stream) {
+    if (!t || !out) return fail(VP3D_ERR_ARG, "NULL argument");
+    if (!t->have_fwd) return fail(VP3D_ERR_STATE, "no forward yet");
+    if (layer < 0 || layer >= (int)t->layers.size() - 1) return fail(VP3D_ERR_ARG, "layer out of range");
+    const int64_t n = (int64_t)t->B * t->len[layer] * t->cfg.channels;
+    if (n_elems != n) return fail(VP3D_ERR_ARG, "n_elems must be rows * channels = " + std::to_string(n));
+    HIP_TRY(launch_relu_mask(t->Z[layer], n, t->cfg.channels, bn_arr(t, layer, 2), bn_arr(t, layer, 3), out,
+                             (hipStream_t)stream));
+    return VP3D_OK;
+}
+
 int vp3d_adam_step(int n, float* const* params, const float* const* grads, float* const* exp_avg,
                    float* const* exp_avg_sq, float* const* max_exp_avg_sq, const int64_t* numel, double lr,
                    double beta1, double beta2, double eps, double weight_decay, int64_t step, int amsgrad,

@@ -49,7 +49,7 @@ EXPORTS = [
     "vp3d_stream_frames_seen", "vp3d_stream_graph_capture", "vp3d_stream_graph_launch",
     "vp3d_stream_destroy",
     "vp3d_trainer_create", "vp3d_trainer_destroy", "vp3d_train_forward", "vp3d_train_backward",
-    "vp3d_train_dropout_mask", "vp3d_train_layer_rows", "vp3d_adam_step", "vp3d_mpjpe_backward",
+    "vp3d_train_dropout_mask", "vp3d_train_relu_mask", "vp3d_train_layer_rows", "vp3d_adam_step", "vp3d_mpjpe_backward",
     "vp3d_seq_weight_count", "vp3d_seq_create", "vp3d_seq_destroy", "vp3d_seq_forward",
     "vp3d_seq_sliding_window",
 ]
@@ -140,6 +140,7 @@ _SIGNATURES = {
                                   ctypes.c_double, ctypes.c_uint64, _vp, _vp]),
     "vp3d_train_backward": (_int, [_vp, ctypes.POINTER(_vp), _int, _vp, ctypes.POINTER(_vp), _vp]),
     "vp3d_train_dropout_mask": (_int, [_vp, _int, _i64, _vp, _vp]),
+    "vp3d_train_relu_mask": (_int, [_vp, _int, _i64, _vp, _vp]),
     "vp3d_train_layer_rows": (_i64, [_vp, _int]),
     "vp3d_adam_step": (_int, [_int, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                               ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),

@@ -89,6 +89,18 @@ class NativeTrainer:
                                                       N.stream_ptr(self.device)), "vp3d_train_dropout_mask")
         return out
 
+    def relu_mask(self, layer: int, channels: int) -> torch.Tensor:
+        """ReLU mask (uint8, rows x channels: BN output > 0) of conv layer `layer` in the latest
+        forward (test hook)."""
+        rows = self.layer_rows(layer)
+        if rows < 0:
+            raise RuntimeError("no train-mode forward yet")
+        out = torch.empty((rows, channels), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_train_relu_mask(self._h, layer, out.numel(), out.data_ptr(),
+                                                   N.stream_ptr(self.device)), "vp3d_train_relu_mask")
+        return out
+
     def close(self) -> None:
         if self._h:
             self._lib.vp3d_trainer_destroy(self._h)

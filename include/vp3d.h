@@ -211,6 +211,12 @@ int vp3d_train_backward(vp3d_trainer* t, float* const* params, int n_params, con
  * layer's output, row-major (b, t, c).  Test hook for the parity tests. */
 int vp3d_train_dropout_mask(vp3d_trainer* t, int layer, int64_t n_elems, uint8_t* out, void* stream);
 
+/* The ReLU mask (1 = BN output > 0) of conv layer `layer` in the latest forward, same
+ * layout as vp3d_train_dropout_mask.  Test hook: an element whose BN output lies within
+ * rounding of 0 may take the other side of the ReLU in another f32 implementation, so the
+ * parity tests feed this mask (with the dropout mask) to the oracle. */
+int vp3d_train_relu_mask(vp3d_trainer* t, int layer, int64_t n_elems, uint8_t* out, void* stream);
+
 /* Row count (B * frames) of conv layer `layer`'s output in the latest forward, or -1. */
 int64_t vp3d_train_layer_rows(const vp3d_trainer* t, int layer);
 

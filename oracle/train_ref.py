@@ -36,13 +36,18 @@ def _mask_cf(mask, B, L):
 
 def lifter_train_forward(params: Dict[str, torch.Tensor], x, filter_widths: Sequence[int], causal=False,
                          strided=False, dense=False, p: float = 0.0,
-                         masks: Optional[List[np.ndarray]] = None, momentum: float = 0.1, eps: float = 1e-5):
+                         masks: Optional[List[np.ndarray]] = None, momentum: float = 0.1, eps: float = 1e-5,
+                         relu_masks: Optional[List[np.ndarray]] = None):
     """Train-mode forward of TemporalModel (strided=False) / TemporalModelOptimized1f.
 
     params: state_dict-keyed tensors; the trainable ones may require grad, the BN
     running statistics are updated in place (F.batch_norm(training=True)).
     masks[l]: keep mask of conv layer l (0 = expand, then the block convs) as
-    (B*L_l, C) uint8 rows, required when p > 0."""
+    (B*L_l, C) uint8 rows, required when p > 0.
+    relu_masks[l] (same layout, optional): take the ReLU decisions of another implementation
+    (x * mask instead of relu(x)): an element whose BN output lies within rounding of 0 may
+    fall on either side in two f32 implementations, and in a small batch one such element
+    moves the BatchNorm gradients of its channel far more than rounding does."""
     xt = torch.as_tensor(np.asarray(x)) if not isinstance(x, torch.Tensor) else x
     B, T = xt.shape[0], xt.shape[1]
     pad, shift, convs = geometry(filter_widths, causal, strided, dense)
@@ -59,9 +64,14 @@ def lifter_train_forward(params: Dict[str, torch.Tensor], x, filter_widths: Sequ
         noise = _mask_cf(masks[layer], B, h.shape[2]).div_(1 - p)
         return h * noise
 
+    def relu(h, layer):
+        if relu_masks is None:
+            return F.relu(h)
+        return h * _mask_cf(relu_masks[layer], B, h.shape[2]).to(h.dtype)
+
     h = xt.reshape(B, T, -1).permute(0, 2, 1)
-    h = drop(F.relu(bn(F.conv1d(h, params["expand_conv.weight"], None, stride=w0 if strided else 1),
-                       "expand_bn")), 0)
+    h = drop(relu(bn(F.conv1d(h, params["expand_conv.weight"], None, stride=w0 if strided else 1),
+                     "expand_bn"), 0), 0)
     for i, (k, d, s) in enumerate(convs):
         if strided:
             w = filter_widths[i + 1]
@@ -69,10 +79,10 @@ def lifter_train_forward(params: Dict[str, torch.Tensor], x, filter_widths: Sequ
         else:
             pd, c = pad[i + 1], shift[i + 1]
             res = h[:, :, pd + c:h.shape[2] - pd + c]
-        h = drop(F.relu(bn(F.conv1d(h, params[f"layers_conv.{2 * i}.weight"], None, stride=s, dilation=d),
-                           f"layers_bn.{2 * i}")), 2 * i + 1)
-        h = res + drop(F.relu(bn(F.conv1d(h, params[f"layers_conv.{2 * i + 1}.weight"], None),
-                                 f"layers_bn.{2 * i + 1}")), 2 * i + 2)
+        h = drop(relu(bn(F.conv1d(h, params[f"layers_conv.{2 * i}.weight"], None, stride=s, dilation=d),
+                         f"layers_bn.{2 * i}"), 2 * i + 1), 2 * i + 1)
+        h = res + drop(relu(bn(F.conv1d(h, params[f"layers_conv.{2 * i + 1}.weight"], None),
+                               f"layers_bn.{2 * i + 1}"), 2 * i + 2), 2 * i + 2)
     h = F.conv1d(h, params["shrink.weight"], params["shrink.bias"])
     return h.permute(0, 2, 1).reshape(B, h.shape[2], -1, 3)
 
