@@ -9,10 +9,11 @@
 //                           projection P is computed once per frame and shared by every
 //                           window that contains the frame (:193-195)
 //   layernorm_kernel        the post-norm LayerNorms of nn.TransformerEncoderLayer
-//   attention_kernel        softmax(q k^T / sqrt(dh)) v per (window, head), K and V of
-//                           the window in LDS, one query per thread (online softmax);
-//                           `last_only`: the last encoder layer only needs the last query
-//                           (CamTransformer.py:201 keeps enc_out[:, -1])
+//   attention_mfma_kernel   softmax(q k^T / sqrt(dh)) v per (window, head) on the f32 MFMA
+//                           (full layers)
+//   attention_last_kernel   the same for the last query only: the last encoder layer only
+//                           needs it (CamTransformer.py:201 keeps enc_out[:, -1])
+//   attention_kernel        scalar fallback (head dims without an MFMA variant)
 //   lstm_kernel             the stacked nn.LSTM recurrence (gate order i, f, g, o; zero
 //                           initial state) of a tile of windows, persistent over all time
 //                           steps; layer 0's input projection is precomputed per frame
