@@ -118,6 +118,9 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
             const int64_t off = g.seq_off[pr.x];
             const int len = g.seq_len[pr.x];
             const int f0 = pr.y - g.lead + t * p.stride;
+            // tap = k / lda without an integer division: k < 2^12 and lda <= 2^11, so
+            // (k + 0.5) * (1 / lda) stays > 1/(4 lda) away from the next integer
+            const float inv_lda = 1.0f / (float)p.lda;
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
                 const int k0 = ks * 32 + (lane >> 4) * 8;
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
                     // lda, f2 and K even: a pair never straddles a tap or the kps|cams edge
                     const int k = k0 + e;
                     const bool in = k < p.K;
-                    const int tap = in ? k / p.lda : 0;
+                    const int tap = in ? (int)(((float)k + 0.5f) * inv_lda) : 0;
                     const int c = in ? k - tap * p.lda : 0;
                     int fr = f0 + tap;
                     fr = fr < 0 ? 0 : (fr >= len ? len - 1 : fr);
