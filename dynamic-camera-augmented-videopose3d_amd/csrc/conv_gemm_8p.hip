@@ -54,7 +54,16 @@ __device__ __forceinline__ void vmw() {
 
 // ABL (ablation, measurement only): 0 = normal, 1 = no LDS-DMA inside the K loop
 // (MFMA + LDS reads on stale data), 2 = no MFMAs (memory traffic only), 3 = no
-// fragment reads after the first K-step (DMA + MFMA), 4 = neither reads nor DMA.
+// fragment reads after the first K-step (DMA + MFMA), 4 = neither reads nor DMA,
+// 7 = normal + per-workgroup timestamps into g_trace (tools/ubench/gemm_check 8pt).
+__device__ unsigned long long* g_trace;
+
+__device__ __forceinline__ void trace_stamp(int wg, int slot) {
+    // 100 MHz wall clock (comparable across CUs)
+    const unsigned long long rt = __builtin_amdgcn_s_memrealtime();
+    if (!g_trace) return;
+    g_trace[(size_t)wg * 10 + slot] = rt;
+}
 template <typename CT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[PRING + 2 * PMAXN * 4];
@@ -77,6 +86,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     const int tile_m = wg / ntn;
     const int tile_n = wg - tile_m * ntn;
     const int m0 = tile_m * PM, n0 = tile_n * PN;
+    if (ABL == 7 && tid == 0 && g_trace) {
+        trace_stamp(blockIdx.x, 0);
+        // slot 4: hardware ids (HW_ID: cu / sh / se; XCC_ID)
+        g_trace[(size_t)blockIdx.x * 10 + 4] =
+            ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+            __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
 
     // LDS-DMA source addressing (as conv_gemm_big.hip): piece q of wave w covers rows
     // (w + 8q)*16 .. +15 of the operand; lane l fills physical chunk (l & 3) of row
@@ -140,6 +156,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scale/shift stores
     barrier_pinned();
+    if (ABL == 7 && tid == 0) trace_stamp(blockIdx.x, 1);
     if (wr == 1) barrier_pinned();  // G1 runs one barrier interval behind G0
 
     u32x4 bf[4], alo[4], ahi[4];
@@ -154,9 +171,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
             for (int i = 0; i < 4; ++i) alo[i] = *(const u32x4*)(slot + a_frag_off + i * 16 * 64);
         }
         if (ABL != 1 && ABL != 4 && s + 2 < nk) issue_a(s + 2);
-        // the residual block of this wave, two K-steps before the end: the tail's
-        // vmcnt(0) in segment B retires it, the epilogue never waits for it
-        if (p.R && s == (nk >= 2 ? nk - 2 : 0)) load_residual_tp<CT, 8>(p, res, m0 + wr * 128, n0 + wc * 64, lane);
+        // the residual block of this wave, two K-steps before the end (buffer loads,
+        // 32-bit offsets: 0 spills); they have the last K-step to land
+        if (p.R && s == (nk >= 2 ? nk - 2 : 0)) load_residual_tp_buf<CT, 8>(p, res, m0 + wr * 128, n0 + wc * 64, lane);
         barrier_pinned();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
@@ -179,8 +196,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
             vmw<6>();  // younger than stage s+1: B(s+2), A(s+2), B(s+3)
         } else if (s + 2 < nk) {
             vmw<4>();  // B(s+2), A(s+2)
-        } else {
-            vmw<0>();
+        } else if (s + 2 == nk) {
+            // stage s+1 is the last one; the 16 residual loads issued in segment A of
+            // this step are younger and stay in flight (the compiler waits for them
+            // before the epilogue reads them)
+            if (p.R) vmw<16>();
+            else vmw<0>();
         }
         barrier_pinned();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -196,12 +217,23 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
         barrier_pinned();
     }
     if (wr == 0) barrier_pinned();  // match G1's extra barrier
+    if (ABL == 7 && tid == 0) trace_stamp(blockIdx.x, 2);
 
     const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.ldy * sizeof(CT)));
     epilogue_tp<CT, 8, true>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc, res);
+    if (ABL == 7) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) trace_stamp(blockIdx.x, 3);
+    }
 }
 
 }  // namespace
+
+// measurement only: where VP3D_ABL=7 launches write their timestamps (10 u64 per workgroup)
+hipError_t conv_gemm_8p_set_trace(unsigned long long* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &buf, sizeof(buf));
+}
 
 bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
     if (compute == Act::F32 || a_type != compute || out_type != compute) return false;
@@ -211,6 +243,7 @@ bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
         (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
         return false;
     if ((size_t)p.M * p.ldy * 2 >= (1u << 31)) return false;  // 32-bit buffer offsets
+    if (p.R && (size_t)((p.M + p.T_out - 1) / p.T_out) * p.R_T * p.ldr * 2 >= (1u << 31)) return false;
     return true;
 }
 
@@ -228,6 +261,8 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 3>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16 && abl == 4)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 4>), grid, dim3(512), 0, stream, p);
+    else if (compute == Act::BF16 && abl == 7)
+        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 7>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16>), grid, dim3(512), 0, stream, p);
     else

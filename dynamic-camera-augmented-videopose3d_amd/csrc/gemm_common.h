@@ -289,8 +289,31 @@ __device__ __forceinline__ void load_residual_tp(const ConvGemmParams& p, u32x4 
     }
 }
 
+// As load_residual_tp, through a buffer resource with 32-bit byte offsets computed at
+// the call (the wave's base row is laundered through an empty asm, so the row
+// arithmetic is not hoisted out of the K loop and held there in 16 address VGPRs;
+// caller: R extent < 2^31 bytes).
+template <typename CT, int MI>
+__device__ __forceinline__ void load_residual_tp_buf(const ConvGemmParams& p, u32x4 (&res)[MI][2], int mw, int nw,
+                                                     int lane) {
+    asm volatile("" : "+v"(mw));
+    const __amdgpu_buffer_rsrc_t r_rsrc = make_rsrc(p.R, 0x7FFFFFFF);
+    const int grp = lane >> 4;
+    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        int m = mw + i * 16 + (lane & 15);
+        m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
+        const int off = (res_row(p, m) * p.ldr + nw + c0) * (int)sizeof(CT);
+        res[i][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_rsrc, off, 0, 0));
+        res[i][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_rsrc, off + 64, 0, 0));
+    }
+}
+
 // PRE: the residual is already in `pre` (load_residual_tp, waited for by the caller).
-template <typename CT, int MI, bool PRE = false>
+// HAS_R: -1 = p.R decides at run time; 0 / 1 = known at compile time (straight-line
+// code, so the compiler's own vmcnt waits before the residual uses stay counted).
+template <typename CT, int MI, bool PRE = false, int HAS_R = -1>
 __device__ __forceinline__ void epilogue_tp(const ConvGemmParams& p, f32x4 (&acc)[MI][4], int mw, int nw,
                                             int lane, const float* s_scale, const float* s_shift,
                                             __amdgpu_buffer_rsrc_t y_rsrc, const u32x4 (*pre)[2] = nullptr) {
@@ -308,7 +331,7 @@ __device__ __forceinline__ void epilogue_tp(const ConvGemmParams& p, f32x4 (&acc
             sh[j][q] = h4[q];
         }
     }
-    const bool has_r = p.R != nullptr;
+    const bool has_r = HAS_R < 0 ? p.R != nullptr : HAS_R == 1;
     u32x4 res[2][2];
     auto load_res = [&](int i, u32x4 (&rr)[2]) {
         int m = mw + i * 16 + (lane & 15);

@@ -64,6 +64,12 @@ hipError_t launch_conv_gemm_tp(const ConvGemmParams& p, Act compute, hipStream_t
 // Wave-group ping-pong 256x256 kernel with register-direct epilogue (conv_gemm_8p.hip).
 bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream);
+// Persistent form of the same kernel (conv_gemm_8pp.hip): one workgroup per CU, one
+// continuous LDS-DMA stream across its tiles (K >= 128).
+bool conv_gemm_8pp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
+hipError_t launch_conv_gemm_8pp(const ConvGemmParams& p, Act compute, hipStream_t stream);
+// measurement only (VP3D_ABL=7 launches): 10 u64 timestamps/ids per workgroup
+hipError_t conv_gemm_8p_set_trace(unsigned long long* buf);
 
 // Window source for a forward that gathers its input on the fly (vp3d_forward_windows):
 // the B windows are frames [start_b - lead, start_b - lead + window) of device-resident

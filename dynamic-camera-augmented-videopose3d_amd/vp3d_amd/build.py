@@ -19,7 +19,7 @@ INCLUDE = os.path.join(REPO, "include")
 BUILD_DIR = os.path.join(ROOT_PKG, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libvp3d.so")
 
-SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_persist.hip", "conv_gemm_pp.hip", "expand_gemm.hip", "conv_gemm_tp.hip", "conv_gemm_8p.hip", "preprocess.hip", "metrics.hip", "stream_step.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp", "vp3d_seq.cpp"]
+SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_persist.hip", "conv_gemm_pp.hip", "expand_gemm.hip", "conv_gemm_tp.hip", "conv_gemm_8p.hip", "conv_gemm_8pp.hip", "preprocess.hip", "metrics.hip", "stream_step.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp", "vp3d_seq.cpp"]
 HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "gemm_common.h"), os.path.join(CSRC, "host.h"),
            os.path.join(INCLUDE, "vp3d.h")]
 ARCH = os.environ.get("VP3D_OFFLOAD_ARCH", "gfx950")

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 #include "kernels.h"
 
@@ -79,10 +80,22 @@ int main(int argc, char** argv) {
     hipMemset(Y, 0, (size_t)M * N * 2);
     p.A = A; p.W = W; p.scale = sc; p.shift = sh; p.R = use_r ? R : nullptr; p.Y = Y;
 
+    const bool trace = !strcmp(kern, "8pt");
+    unsigned long long* d_trace = nullptr;
+    const int nwg_trace = ((M + 255) / 256) * (N / 256);
+    if (trace) {
+        // the buffer is in place before the first launch (VP3D_ABL=7 launches write it)
+        hipMalloc(&d_trace, (size_t)nwg_trace * 80);
+        hipMemset(d_trace, 0, (size_t)nwg_trace * 80);
+        if (conv_gemm_8p_set_trace(d_trace) != hipSuccess) { printf("set_trace failed\n"); return 1; }
+        setenv("VP3D_ABL", "7", 1);
+        kern = "8p";
+    }
     auto launch = [&]() -> hipError_t {
         if (!strcmp(kern, "tp")) return launch_conv_gemm_tp(p, Act::BF16, 0);
         if (!strcmp(kern, "big")) return launch_conv_gemm_big(p, Act::BF16, Act::BF16, 0);
         if (!strcmp(kern, "8p")) return launch_conv_gemm_8p(p, Act::BF16, 0);
+        if (!strcmp(kern, "8pp")) return launch_conv_gemm_8pp(p, Act::BF16, 0);
         if (!strcmp(kern, "persist")) return launch_conv_gemm_persist(p, Act::BF16, Act::BF16, 0);
         return launch_conv_gemm(p, Act::BF16, Act::BF16, Act::BF16, 0);
     };
@@ -120,6 +133,59 @@ int main(int argc, char** argv) {
     }
     printf("%s M=%d N=%d K=%d dil=%d res=%d: max|d|=%.4g  bad=%ld of %ld\n", kern, M, N, K, dil, use_r, maxe,
            bad, (long)M * N);
+    if (trace) {
+        // one traced launch: per-workgroup start / prologue done / K loop done / stores
+        // retired (100 MHz wall clock), grouped by the CU each workgroup ran on
+        const int nwg = nwg_trace;
+        unsigned long long* d = d_trace;
+        for (int i = 0; i < 3; ++i) launch();
+        hipDeviceSynchronize();
+        std::vector<unsigned long long> t((size_t)nwg * 10);
+        hipMemcpy(t.data(), d, t.size() * 8, hipMemcpyDeviceToHost);
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int w = 0; w < nwg; ++w) { t0 = std::min(t0, t[w * 10]); t1 = std::max(t1, t[w * 10 + 3]); }
+        double pro = 0, loop = 0, epi = 0, cpro = 0, cloop = 0, cepi = 0;
+        for (int w = 0; w < nwg; ++w) {
+            const unsigned long long* r = &t[w * 10];
+            pro += r[1] - r[0]; loop += r[2] - r[1]; epi += r[3] - r[2];
+            cpro += r[6] - r[5]; cloop += r[7] - r[6]; cepi += r[8] - r[7];
+        }
+        printf("trace: kernel span %.1f us; per WG mean: prologue %.2f us, K loop %.2f us, epilogue %.2f us"
+               " (cycles %.0f / %.0f / %.0f -> %.2f GHz in loop)\n", (t1 - t0) / 100.0, pro / nwg / 100.0,
+               loop / nwg / 100.0, epi / nwg / 100.0, cpro / nwg, cloop / nwg, cepi / nwg,
+               cloop / (loop / 100.0) / 1e3);
+        // per CU: sorted workgroups, gaps between one's end and the next's start
+        std::vector<std::pair<unsigned long long, int>> key;
+        for (int w = 0; w < nwg; ++w) key.push_back({(t[w * 10 + 4] & 0xFFFFFFFF0000FF00ull) , w});
+        std::sort(key.begin(), key.end(), [&](auto& x, auto& y) {
+            return x.first != y.first ? x.first < y.first : t[x.second * 10] < t[y.second * 10]; });
+        double gap = 0; long ng = 0; int ncu = 0;
+        for (size_t i = 0; i < key.size(); ++i) {
+            if (i == 0 || key[i].first != key[i - 1].first) { ++ncu; continue; }
+            gap += (double)t[key[i].second * 10] - (double)t[key[i - 1].second * 10 + 3]; ++ng;
+        }
+        printf("trace: %d distinct CUs, mean gap end->next start on a CU %.2f us (%ld gaps)\n", ncu,
+               ng ? gap / ng / 100.0 : 0.0, ng);
+        // round-by-round: start times of the i-th workgroup on each CU, relative to t0
+        for (int round = 0; round < 16; ++round) {
+            double smin = 1e30, smax = 0, emin = 1e30, emax = 0; int cnt = 0;
+            size_t i = 0;
+            while (i < key.size()) {
+                size_t j = i; while (j < key.size() && key[j].first == key[i].first) ++j;
+                if (i + round < j) {
+                    const unsigned long long* r = &t[key[i + round].second * 10];
+                    smin = std::min(smin, (double)(r[0] - t0)); smax = std::max(smax, (double)(r[0] - t0));
+                    emin = std::min(emin, (double)(r[3] - t0)); emax = std::max(emax, (double)(r[3] - t0));
+                    ++cnt;
+                }
+                i = j;
+            }
+            if (!cnt) break;
+            printf("  round %2d: %3d WGs start %.1f..%.1f us, end %.1f..%.1f us\n", round, cnt, smin / 100,
+                   smax / 100, emin / 100, emax / 100);
+        }
+        return 0;
+    }
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     for (int i = 0; i < 3; ++i) launch();
