@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="approximate CPU-baseline sample duration (0 disables)")
     ap.add_argument("--parity-windows", type=int, default=32)
+    ap.add_argument("--settle-seconds", type=float, default=0.5,
+                    help="untimed steps after --warmup until the device has run this long")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = 1024 if args.train else (16384 if args.seq_model else 65536 if args.sequence else 8192)
@@ -544,6 +546,15 @@ def main():
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
+        # then untimed steps until the device has been busy for ~0.5 s: after a cold
+        # start (the trajectory setup leaves the GPU idle for seconds) the step period
+        # falls from ~5.8 to ~3.2 ms over the first ~20 steps as the clocks ramp
+        # (profiles/r01f_traj_step_ramp.txt), which a 5-step warm-up does not cover
+        torch.cuda.synchronize()
+        t_settle = time.perf_counter()
+        while time.perf_counter() - t_settle < args.settle_seconds:
+            step()
+            torch.cuda.synchronize()
         # per-layer times from an untimed pass with events around every launch; the timed
         # loop below carries events around the dominant layer only (events on all ten
         # launches cost ~75 us per step)
