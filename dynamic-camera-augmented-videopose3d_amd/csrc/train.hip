@@ -13,6 +13,7 @@
 // The data are channel-last rows (B*L, C) as everywhere in this library.  All
 // arithmetic is f32 (the reference trains in fp32); per-channel reductions are
 // accumulated in f64.
+#include <climits>
 #include "kernels.h"
 
 #pragma clang fp contract(off)
@@ -207,9 +208,10 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
                                                          int R_stride, int R_off, float* __restrict__ Y) {
     const int c4 = C >> 2;
     const int64_t total = M * c4;
+    const bool small = total < INT32_MAX;  // 32-bit row / frame arithmetic
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t m = e / c4;
+        const int64_t m = small ? (int64_t)((uint32_t)e / (uint32_t)c4) : e / c4;
         const int c = (int)(e - m * c4) * 4;
         const f32x4 z = *(const f32x4*)(Z + m * C + c);
         const f32x4 al = *(const f32x4*)(alpha + c);
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const float* __restrict
             o[j] = v;
         }
         if (R) {
-            const int64_t b = m / T_out, t = m - b * T_out;
+            const int64_t b = small ? (int64_t)((uint32_t)m / (uint32_t)T_out) : m / T_out, t = m - b * T_out;
             const f32x4 r = *(const f32x4*)(R + (b * R_T + t * R_stride + R_off) * C + c);
 #pragma unroll
             for (int j = 0; j < 4; ++j) o[j] = r[j] + o[j];
@@ -242,29 +244,36 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restri
                                                            const float* __restrict__ coef, float dscale,
                                                            uint64_t seed, uint64_t thresh, int layer, int T_out,
                                                            int dz_T, int dz_off, float* __restrict__ dZ) {
+    // per-channel operands as float4 (C % 4 == 0, 16-byte aligned: launch_bn_train_backward)
     const int c4 = C >> 2;
     const int64_t total = M * c4;
+    const bool small = total < INT32_MAX;
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t m = e / c4;
+        const int64_t m = small ? (int64_t)((uint32_t)e / (uint32_t)c4) : e / c4;
         const int c = (int)(e - m * c4) * 4;
         const f32x4 z = *(const f32x4*)(Z + m * C + c);
         const f32x4 d = *(const f32x4*)(dO + m * C + c);
+        const f32x4 al = *(const f32x4*)(alpha + c);
+        const f32x4 sh = *(const f32x4*)(shift + c);
+        const f32x4 mu = *(const f32x4*)(mean + c);
+        const f32x4 k0 = *(const f32x4*)(coef + c);
+        const f32x4 k1 = *(const f32x4*)(coef + C + c);
+        const f32x4 k2 = *(const f32x4*)(coef + 2 * C + c);
         f32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int cc = c + j;
-            const float y = z[j] * alpha[cc] + shift[cc];
+            const float y = z[j] * al[j] + sh[j];
             float g = 0.f;
             if (y > 0.f) {
                 g = d[j];
-                if (thresh != (1ull << 32)) g = drop_keep(seed, layer, m * C + cc, thresh) ? g * dscale : 0.f;
+                if (thresh != (1ull << 32)) g = drop_keep(seed, layer, m * C + c + j, thresh) ? g * dscale : 0.f;
             }
-            const float xm = z[j] - mean[cc];
-            const float v = (g - coef[cc]) - xm * coef[C + cc];
-            o[j] = v * coef[2 * C + cc];
+            const float xm = z[j] - mu[j];
+            const float v = (g - k0[j]) - xm * k1[j];
+            o[j] = v * k2[j];
         }
-        const int64_t b = m / T_out, t = m - b * T_out;
+        const int64_t b = small ? (int64_t)((uint32_t)m / (uint32_t)T_out) : m / T_out, t = m - b * T_out;
         *(f32x4*)(dZ + (b * dz_T + t + dz_off) * C + c) = o;
     }
 }
