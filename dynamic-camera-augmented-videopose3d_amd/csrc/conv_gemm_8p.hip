@@ -64,7 +64,7 @@ __device__ __forceinline__ void trace_stamp(int wg, int slot) {
     if (!g_trace) return;
     g_trace[(size_t)wg * 10 + slot] = rt;
 }
-template <typename CT, int ABL = 0>
+template <typename CT, int ABL = 0, bool NT = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[PRING + 2 * PMAXN * 4];
     float* const s_scale = (float*)(smem + PRING);
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     if (ABL == 7 && tid == 0) trace_stamp(blockIdx.x, 2);
 
     const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.ldy * sizeof(CT)));
-    epilogue_tp<CT, 8, true>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc, res);
+    epilogue_tp<CT, 8, true, -1, NT ? 2 : 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc, res);
     if (ABL == 7) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -247,6 +247,15 @@ bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
     return true;
 }
 
+// VP3D_GEMM_NT=1: nontemporal output stores (A/B)
+static bool gemm_nt() {
+    static const bool v = [] {
+        const char* e = getenv("VP3D_GEMM_NT");
+        return e && atoi(e) != 0;
+    }();
+    return v;
+}
+
 hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream) {
     const dim3 grid(((p.M + PM - 1) / PM) * (p.N / PN));
     static const int abl = [] {
@@ -263,6 +272,8 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 4>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16 && abl == 7)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 7>), grid, dim3(512), 0, stream, p);
+    else if (compute == Act::BF16 && gemm_nt())
+        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 0, true>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16>), grid, dim3(512), 0, stream, p);
     else

@@ -49,7 +49,7 @@ __device__ __forceinline__ int exp_swz(int r, int c) { return r * 4 + ((c + 2 * 
 // GATHER: the input rows are not a (B, T, Cin) tensor but windows of device-resident
 // sequences, gathered here (GatherSrc, kernels.h): the ChunkedGenerator batch and the
 // camera concat fused into the operand loader.
-template <typename CT, int NKS, int RB, bool GATHER>
+template <typename CT, int NKS, int RB, bool GATHER, bool NT = false>
 __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
     constexpr int kExpRowsPerWave = 16 * RB;
     constexpr int kExpRows = kExpRowsPerWave * kExpWaves;
@@ -207,25 +207,53 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
             const int c16 = lane & 7;
             const u32x4 v = stage[row * 8 + (c16 ^ (row & 7))];
             const int m = m_wave + row;
-            if (m < p.M) *(u32x4*)(Y + (int64_t)m * p.ldy + n0 + c16 * 8) = v;
+            if (m < p.M) {
+                u32x4* dst = (u32x4*)(Y + (int64_t)m * p.ldy + n0 + c16 * 8);
+                if constexpr (NT)
+                    __builtin_nontemporal_store(v, dst);
+                else
+                    *dst = v;
+            }
         }
         asm volatile("" ::: "memory");
         __syncthreads();
     }
 }
 
-template <typename CT, int RB, bool GATHER>
-hipError_t launch_rb(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
+// Output stores: nontemporal (nt) by default when the output exceeds the 256 MB Infinity
+// Cache; VP3D_EXPAND_NT=0 for default-policy stores.
+// The 1.36 GB output (B = 8192) cannot stay in the 256 MB Infinity Cache anyway; streamed
+// past it, it leaves the caches to the weights and the block-1 conv that follows runs
+// 1-1.5 % faster (3.10-3.12 vs 3.14-3.18 ms per step, A/B on one box).
+bool expand_nt() {
+    static const bool v = [] {
+        const char* e = getenv("VP3D_EXPAND_NT");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
+template <typename CT, int RB, bool GATHER, bool NT>
+hipError_t launch_rb_nt(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     const dim3 grid((p.M + 64 * RB - 1) / (64 * RB));
     switch (nks) {
-        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
-        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
-        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
-        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
-        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB, GATHER>), grid, dim3(256), 0, s, p, g); break;
+        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
+        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
+        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
+        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
+        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+template <typename CT, int RB, bool GATHER>
+hipError_t launch_rb(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
+    // only outputs larger than the Infinity Cache; a smaller one is better left cached for
+    // the next layer
+    const bool nt = expand_nt() && (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
+    return nt ? launch_rb_nt<CT, RB, GATHER, true>(p, g, nks, s)
+                       : launch_rb_nt<CT, RB, GATHER, false>(p, g, nks, s);
 }
 
 // Row blocks of 16 per wave (VP3D_EXPAND_RB = 1, 2 or 4): fewer rows per wave, fewer
