@@ -256,22 +256,29 @@ hipError_t launch_rb(const ConvGemmParams& p, const GatherSrc& g, int nks, hipSt
                        : launch_rb_nt<CT, RB, GATHER, false>(p, g, nks, s);
 }
 
-// Row blocks of 16 per wave (VP3D_EXPAND_RB = 1, 2 or 4): fewer rows per wave, fewer
-// VGPRs and less LDS per workgroup, more resident waves to hide store / input latency.
-int expand_rb() {
-    static const int v = [] {
+// Row blocks of 16 per wave (VP3D_EXPAND_RB = 1..4 forces one): fewer rows per wave, fewer
+// VGPRs and less LDS per workgroup, more resident waves to hide store / input latency, but
+// the weight sweep is repeated for every workgroup.  Default: 4 where that instantiation
+// still holds 2 waves per SIMD (<= 256 VGPR + AGPR: the plain loader with K <= 128 — 250),
+// else 2 (the gathered loader's address arithmetic, or K up to 160, put RB = 4 at 280-327
+// registers = 1 wave per SIMD).  Measured at B = 8192: plain K = 102: 4 -> 0.370, 2 ->
+// 0.406, 1 -> 0.442 ms; gathered K = 138 (config 3): 4 -> 0.548, 3 -> 0.557, 2 -> 0.400 ms.
+int expand_rb(int nks, bool gather) {
+    static const int forced = [] {
         const char* e = getenv("VP3D_EXPAND_RB");
-        const int r = e ? atoi(e) : 4;  // measured at B = 8192: 4 -> 0.370, 2 -> 0.406, 1 -> 0.442 ms
-        return (r == 1 || r == 2 || r == 4) ? r : 4;
+        const int r = e ? atoi(e) : 0;
+        return (r >= 1 && r <= 4) ? r : 0;
     }();
-    return v;
+    if (forced) return forced;
+    return (!gather && nks <= 4) ? 4 : 2;
 }
 
 template <typename CT, bool GATHER>
 hipError_t launch_t(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
-    switch (expand_rb()) {
+    switch (expand_rb(nks, GATHER)) {
         case 1: return launch_rb<CT, 1, GATHER>(p, g, nks, s);
         case 2: return launch_rb<CT, 2, GATHER>(p, g, nks, s);
+        case 3: return launch_rb<CT, 3, GATHER>(p, g, nks, s);
         default: return launch_rb<CT, 4, GATHER>(p, g, nks, s);
     }
 }
