@@ -247,13 +247,14 @@ bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
     return true;
 }
 
-// VP3D_GEMM_NT=1: nontemporal output stores (A/B)
-static bool gemm_nt() {
-    static const bool v = [] {
+// VP3D_GEMM_NT=1: nontemporal output stores on every layer, 2: on outputs larger than
+// the 256 MB Infinity Cache only (A/B)
+static bool gemm_nt(const ConvGemmParams& p) {
+    static const int v = [] {
         const char* e = getenv("VP3D_GEMM_NT");
-        return e && atoi(e) != 0;
+        return e ? atoi(e) : 0;
     }();
-    return v;
+    return v == 1 || (v == 2 && (int64_t)p.M * p.ldy * 2 > ((int64_t)256 << 20));
 }
 
 hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream) {
@@ -272,7 +273,7 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 4>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16 && abl == 7)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 7>), grid, dim3(512), 0, stream, p);
-    else if (compute == Act::BF16 && gemm_nt())
+    else if (compute == Act::BF16 && gemm_nt(p))
         hipLaunchKernelGGL((conv_gemm_8p<__bf16, 0, true>), grid, dim3(512), 0, stream, p);
     else if (compute == Act::BF16)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16>), grid, dim3(512), 0, stream, p);
