@@ -233,16 +233,17 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
     const int64_t row0 = (int64_t)w * W;
     const int ld = 3 * d;
     const int nkb = (W + 15) / 16;
-    for (int e = threadIdx.x; e < nkb * 16 * DH; e += blockDim.x) {
-        const int j = e / DH, c = e - j * DH;
-        float kv = 0.f, vv = 0.f;
+    // K, V rows of the window as 16-byte pieces (d, DH multiples of 4: launch_attention)
+    for (int e = threadIdx.x; e < nkb * 16 * (DH / 4); e += blockDim.x) {
+        const int j = e / (DH / 4), c = (e - j * (DH / 4)) * 4;
+        f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
         if (j < W) {
             const float* r = QKV + (row0 + j) * ld + h * DH + c;
-            kv = r[d];
-            vv = r[2 * d];
+            kv = *(const f32x4*)(r + d);
+            vv = *(const f32x4*)(r + 2 * d);
         }
-        Ks[j * ATT_LD + c] = kv;
-        Vs[j * ATT_LD + c] = vv;
+        *(f32x4*)&Ks[j * ATT_LD + c] = kv;
+        *(f32x4*)&Vs[j * ATT_LD + c] = vv;
     }
     __syncthreads();
     const int g = lane >> 4, lq = lane & 15;
@@ -286,9 +287,13 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         }
         l += __shfl_xor(l, 16, 64);
         l += __shfl_xor(l, 32, 64);
-        f32x4 o[DH / 16];
+        // P.V with one accumulator per (r, ib): 4 * DH/16 independent MFMA chains instead
+        // of DH/16 chains of 4 * nkb dependent MFMAs (the chain latency bounded the kernel)
+        f32x4 o4[4][DH / 16];
 #pragma unroll
-        for (int ib = 0; ib < DH / 16; ++ib) o[ib] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int ib = 0; ib < DH / 16; ++ib) o4[r][ib] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kb = 0; kb < ATT_WMAX / 16; ++kb) {
             if (kb < nkb) {
@@ -297,10 +302,13 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
                     const float* vr = Vs + (kb * 16 + 4 * g + r) * ATT_LD + lq;
 #pragma unroll
                     for (int ib = 0; ib < DH / 16; ++ib)
-                        o[ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[ib * 16], S[kb][r], o[ib], 0, 0, 0);
+                        o4[r][ib] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[ib * 16], S[kb][r], o4[r][ib], 0, 0, 0);
                 }
             }
         }
+        f32x4 o[DH / 16];
+#pragma unroll
+        for (int ib = 0; ib < DH / 16; ++ib) o[ib] = (o4[0][ib] + o4[1][ib]) + (o4[2][ib] + o4[3][ib]);
         // o[ib][r]: dim ib*16 + 4g + r of query qt*16 + lq
         if (q < W) {
             const float inv = 1.0f / l;
