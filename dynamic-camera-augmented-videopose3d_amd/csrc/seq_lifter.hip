@@ -256,19 +256,27 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         for (int s = 0; s < NS; ++s) qf[s] = qr[4 * s + g] * scale;
         f32x4 S[ATT_WMAX / 16];
         float mx = -INFINITY;
+        // two key blocks per pass: two independent MFMA chains (rows past W of the last
+        // block read zeroed LDS rows and are masked below)
 #pragma unroll
-        for (int kb = 0; kb < ATT_WMAX / 16; ++kb) {
+        for (int kb = 0; kb < ATT_WMAX / 16; kb += 2) {
             if (kb < nkb) {
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
                 const float* kr = Ks + (kb * 16 + lq) * ATT_LD + g;
 #pragma unroll
-                for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[4 * s], qf[s], acc, 0, 0, 0);
+                for (int s = 0; s < NS; ++s) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[4 * s], qf[s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[16 * ATT_LD + 4 * s], qf[s], acc1, 0, 0, 0);
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    if (kb * 16 + 4 * g + r >= W) acc[r] = -INFINITY;
-                    mx = fmaxf(mx, acc[r]);
+                    if (kb * 16 + 4 * g + r >= W) acc0[r] = -INFINITY;
+                    if ((kb + 1) * 16 + 4 * g + r >= W) acc1[r] = -INFINITY;
+                    mx = fmaxf(mx, acc0[r]);
+                    mx = fmaxf(mx, acc1[r]);
                 }
-                S[kb] = acc;
+                S[kb] = acc0;
+                S[kb + 1] = acc1;
             }
         }
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
