@@ -496,6 +496,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # the CPU baseline is a single-GPU (N = 1) figure: under torchrun every rank gets
+        # OMP_NUM_THREADS=1 and the node's cores are shared by N processes
+        args.cpu_seconds = 0.0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.stream or args.train or args.seq_model or args.sequence:
