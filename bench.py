@@ -494,8 +494,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # VP3D_BENCH_REHEARSE=1: rehearse the N-rank path on a box with fewer GPUs (ranks share
+    # devices round-robin, gloo instead of RCCL); never used for reported numbers
+    rehearse = os.environ.get("VP3D_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         # the CPU baseline is a single-GPU (N = 1) figure: under torchrun every rank gets
         # OMP_NUM_THREADS=1 and the node's cores are shared by N processes
         args.cpu_seconds = 0.0
