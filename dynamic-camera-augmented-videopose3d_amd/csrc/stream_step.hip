@@ -77,15 +77,32 @@ __global__ __launch_bounds__(256) void stream_gemv(StreamLayerParams q) {
         }
     }
 
-    // 2. stage the input vector: tap k reads stream time t - (taps-1-k)*dil, clamped at 0
+    // per-row epilogue operands do not depend on the stream position either
+    float sc = 0.f, sh = 0.f;
+    if (n < q.N && lane == 0) {
+        sc = q.scale[n];
+        sh = q.shift[n];
+    }
+
+    // 2. stage the input vector: tap k reads stream time t - (taps-1-k)*dil, clamped at 0.
+    //    A plain (non-ring) input does not depend on t: its loads go out before t arrives,
+    //    so the two memory round trips overlap instead of chaining.
+    const bool plain = !q.in_R && !q.in_frame;
+    if (plain)
+        for (int kk = tid; kk < q.taps * q.cin; kk += blockDim.x) v[kk] = q.in[kk % q.cin];
     const int t = *q.frames_seen;
+    // the residual row of this step (lane 0 of each wave), loaded ahead of the dot product
+    float rv = 0.f;
+    if (q.res && n < q.N && lane == 0) rv = q.res[(int64_t)(q.res_R ? (t & (q.res_R - 1)) : 0) * q.N + n];
     const float* frame = q.in_frame ? q.in_frame + (int64_t)(t & (q.in_frame_R - 1)) * q.cin : nullptr;
-    for (int tap = 0; tap < q.taps; ++tap) {
-        int tt = t - (q.taps - 1 - tap) * q.dil;
-        tt = tt < 0 ? 0 : tt;
-        const float* src = (frame && tt == t) ? frame
-                           : (q.in_R ? q.in + (int64_t)(tt & (q.in_R - 1)) * q.cin : q.in);
-        for (int c = tid; c < q.cin; c += blockDim.x) v[tap * q.cin + c] = src[c];
+    if (!plain) {
+        for (int tap = 0; tap < q.taps; ++tap) {
+            int tt = t - (q.taps - 1 - tap) * q.dil;
+            tt = tt < 0 ? 0 : tt;
+            const float* src = (frame && tt == t) ? frame
+                               : (q.in_R ? q.in + (int64_t)(tt & (q.in_R - 1)) * q.cin : q.in);
+            for (int c = tid; c < q.cin; c += blockDim.x) v[tap * q.cin + c] = src[c];
+        }
     }
     for (int kk = q.K + tid; kk < q.Kp; kk += blockDim.x) v[kk] = 0.f;
     // the expand layer also appends the new frame to its input ring (slot of time t;
@@ -123,9 +140,9 @@ __global__ __launch_bounds__(256) void stream_gemv(StreamLayerParams q) {
         }
         s = wave_sum(s);
         if (lane == 0) {
-            float y = s * q.scale[n] + q.shift[n];
+            float y = s * sc + sh;
             if (q.relu) y = y > 0.f ? y : 0.f;
-            if (q.res) y += q.res[(int64_t)(q.res_R ? (t & (q.res_R - 1)) : 0) * q.N + n];
+            if (q.res) y += rv;
             const int64_t o = q.out_R ? (int64_t)(t & (q.out_R - 1)) * q.N + n : n;
             q.out[o] = y;
         }
