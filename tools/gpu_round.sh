@@ -28,3 +28,13 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $OUT/pmc_$C -o run -- python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --parity-windows 4 > $OUT/pmc_$C.log 2>&1 || exit $?
   echo "pmc $C ok"
 done
+timeout -k 10 300 python bench.py --train --steps 5 --warmup 2 > $OUT/bench_train.log 2>&1 || exit $?
+echo "train:  $(tail -1 $OUT/bench_train.log | cut -c1-200)"
+timeout -k 10 300 python bench.py --seq-model transformer --steps 5 --warmup 2 > $OUT/bench_seq_transformer.log 2>&1 || exit $?
+echo "tf:     $(tail -1 $OUT/bench_seq_transformer.log | cut -c1-200)"
+timeout -k 10 300 python bench.py --seq-model lstm --steps 5 --warmup 2 > $OUT/bench_seq_lstm.log 2>&1 || exit $?
+echo "lstm:   $(tail -1 $OUT/bench_seq_lstm.log | cut -c1-200)"
+timeout -k 10 300 python bench.py --sequence --steps 10 --warmup 3 > $OUT/bench_sequence.log 2>&1 || exit $?
+echo "seq:    $(tail -1 $OUT/bench_sequence.log | cut -c1-200)"
+timeout -k 10 120 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1 || exit $?
+echo "smoke:  $(tail -1 $OUT/smoke.log)"
