@@ -327,15 +327,18 @@ int gemm_8p_mode() {
         const char* e = getenv("VP3D_GEMM");
         if (!e) return 1;
         if (strcmp(e, "8pp") == 0) return 3;
+        if (strcmp(e, "8pd") == 0) return 4;
         return strcmp(e, "8p") == 0 ? 2 : 0;
     }();
     return v;
 }
 // VP3D_GEMM=8pp: the persistent ping-pong kernel (conv_gemm_8pp.hip) wherever 8p runs
-bool gemm_8pp_env() { return gemm_8p_mode() == 3; }
+bool gemm_8pp_env() { return gemm_8p_mode() == 3 || gemm_8p_mode() == 4; }
+// VP3D_GEMM=8pd: the persistent kernel with per-XCD dynamic tile queues
+bool gemm_8pd_env() { return gemm_8p_mode() == 4; }
 bool gemm_8p_env(const ConvGemmParams& p) {
     const int m = gemm_8p_mode();
-    if (m == 3) return true;
+    if (m == 3 || m == 4) return true;
     // default: the ping-pong kernel for contiguous-tap convs (the strided k3 convs and,
     // since its residual preload stopped spilling, the 1x1 convs with a residual: block 1
     // at B = 8192 0.54 vs 0.59 ms on the LDS-ring kernel); the dilated k3 convs (taps
@@ -453,7 +456,7 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_8p_eligible(p, a_type, out_type, compute)) {
         if (gemm_8pp_env() && conv_gemm_8pp_eligible(p, a_type, out_type, compute))
-            return launch_conv_gemm_8pp(p, compute, stream);
+            return launch_conv_gemm_8pp(p, compute, stream, gemm_8pd_env());
         return launch_conv_gemm_8p(p, compute, stream);
     }
     if (conv_gemm_big_eligible(p, a_type, out_type, compute))

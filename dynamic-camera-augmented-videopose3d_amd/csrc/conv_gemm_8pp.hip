@@ -53,9 +53,17 @@ __device__ __forceinline__ void vmw() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename CT, bool HAS_R>
-__global__ __launch_bounds__(512, 1) void conv_gemm_8pp(ConvGemmParams p) {
+// DYN: tiles handed out by per-XCD atomic queues (ctr[0..7]; ctr[8] counts retired
+// workgroups, the last one resets the queues for the next launch) instead of the static
+// blockIdx.x + it*G walk: a CU that runs fast takes more tiles, as under the hardware
+// dispatcher of the non-persistent kernel.  XCD x owns the tiles xcd_remap gives it
+// (base_x + k, k < cnt_x); its workgroups start at k = b>>3 and b>>3 + G/8 and then take
+// k = 2G/8 + atomicAdd(ctr[x], 1), two tiles ahead (the next tile's A rows and B pieces
+// are issued during the current one).
+template <typename CT, bool HAS_R, bool DYN = false>
+__global__ __launch_bounds__(512, 1) void conv_gemm_8pp(ConvGemmParams p, unsigned* ctr) {
     __shared__ __attribute__((aligned(16))) char smem[PRING + 2 * PMAXN * 4];
+    __shared__ int s_fetch;
     float* const s_scale = (float*)(smem + PRING);
     float* const s_shift = s_scale + PMAXN;
 
@@ -84,6 +92,17 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8pp(ConvGemmParams p) {
         m0 = tm * PM;
         n0 = (wg - tm * ntn) * PN;
     };
+    // DYN: tile k of this workgroup's XCD (same tiles xcd_remap assigns to the XCD)
+    const int xcd = (int)blockIdx.x & 7;
+    const int xq = ntiles >> 3, xr = ntiles & 7;
+    const int xbase = (xcd < xr) ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq;
+    const int xcnt = (xcd < xr) ? xq + 1 : xq;
+    auto tile_k = [&](int k, int& m0, int& n0) __attribute__((always_inline)) {
+        const int wg = xbase + k;
+        const int tm = wg / ntn;
+        m0 = tm * PM;
+        n0 = (wg - tm * ntn) * PN;
+    };
 
     const int dma_row = lane >> 2;
     const int dma_c = ((lane & 3) - 2 * ((lane >> 4) & 3)) & 3;
@@ -107,7 +126,23 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8pp(ConvGemmParams p) {
             dst[q] = src_row(p, m);
         }
     };
-    a_rows(0, a_src);
+    auto a_rows_k = [&](int k, int (&dst)[2]) __attribute__((always_inline)) {
+        int m0, n0;
+        tile_k(k, m0, n0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            int m = m0 + (wid + 8 * q) * 16 + dma_row;
+            m = m < p.M ? m : p.M - 1;
+            dst[q] = src_row(p, m);
+        }
+    };
+    const int gx = G >> 3;
+    int k_cur = (int)blockIdx.x >> 3;
+    int k_nxt = k_cur + gx < xcnt ? k_cur + gx : -1;
+    if constexpr (DYN)
+        a_rows_k(k_cur, a_src);
+    else
+        a_rows(0, a_src);
     auto issue_a = [&](int x) __attribute__((always_inline)) {
         const int it = x / nk;
         const int s = x - it * nk;
@@ -124,11 +159,17 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8pp(ConvGemmParams p) {
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(A + (int64_t)(a_src[q] + tap * p.dil) * p.lda + cin),
                                              (lds_ptr_t)(slot + (wid + 8 * q) * 1024), 16, 0, 0);
     };
+    int it_cur = 0;  // DYN: index of the tile being computed
     auto issue_b = [&](int x) __attribute__((always_inline)) {
         const int it = x / nk;
         const int s = x - it * nk;
         int m0, n0;
-        tile_of(it, m0, n0);
+        if constexpr (DYN) {
+            // stages of the current tile (it == it_cur) or of the next one
+            tile_k(it == it_cur ? k_cur : k_nxt, m0, n0);
+        } else {
+            tile_of(it, m0, n0);
+        }
         char* slot = smem + (x % PSLOTS) * PSLOT_BYTES + PM * PK * 2;
         const CT* wb = W + (int64_t)n0 * p.Kp + s * PK;
 #pragma unroll
@@ -216,6 +257,59 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8pp(ConvGemmParams p) {
     using W_NONE = std::integral_constant<int, -1>;
 
     int x = 0;
+    if constexpr (DYN) {
+        while (k_nxt >= 0) {
+            // a tile with a successor: fetch the one after it.  The atomic is issued
+            // here and its value consumed after K-step 1 (by then the counted vmcnt waits
+            // have retired it; it only adds one younger op to them, so they wait a little
+            // more, never less), published through LDS and read after the last K-step.
+            int m0, n0;
+            tile_k(k_cur, m0, n0);
+            unsigned fetched = 0;
+            if (tid == 0) fetched = atomicAdd(&ctr[xcd], 1u);
+            a_rows_k(k_nxt, a_next);
+            step(x, W_STREAM{}, true, true, it_cur > 0, m0, n0);
+            ++x;
+            for (int s = 1; s < nk; ++s, ++x) {
+                step(x, std::integral_constant<int, 6>{}, true, true, false, m0, n0);
+                if (s == 1 && tid == 0) {
+                    s_fetch = 2 * gx + (int)fetched;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                }
+            }
+            int k_after = __builtin_amdgcn_readfirstlane(s_fetch);  // wave-uniform: SGPR
+            k_after = k_after < xcnt ? k_after : -1;
+            epilogue_tp<CT, 8, false, HAS_R ? 1 : 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift,
+                                                     y_rsrc);
+            zero_acc();
+            k_cur = k_nxt;
+            k_nxt = k_after;
+            ++it_cur;
+        }
+        {
+            // the last tile: the stream runs out (x + 3 == T at s = nk-3)
+            int m0, n0;
+            tile_k(k_cur, m0, n0);
+            step(x, W_STREAM{}, true, true, it_cur > 0, m0, n0);
+            ++x;
+            for (int s = 1; s < nk - 3; ++s, ++x) step(x, std::integral_constant<int, 6>{}, true, true, false, m0, n0);
+            step(x, std::integral_constant<int, 4>{}, true, false, false, m0, n0);
+            step(x + 1, std::integral_constant<int, 0>{}, false, false, false, m0, n0);
+            step(x + 2, W_NONE{}, false, false, false, m0, n0);
+            epilogue_tp<CT, 8, false, HAS_R ? 1 : 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift,
+                                                     y_rsrc);
+        }
+        if (wr == 0) barrier_pinned();  // match G1's extra barrier
+        // retire: the last workgroup out resets the queues for the next launch
+        if (tid == 0) {
+            const unsigned done = atomicAdd(&ctr[8], 1u);
+            if (done == (unsigned)G - 1) {
+                for (int i = 0; i < 8; ++i) __hip_atomic_store(&ctr[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctr[8], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        return;
+    }
     // all tiles but the last: every refill exists.  The residual is loaded inside the
     // epilogue (pipelined one 16-row block ahead): held in registers through the last
     // K-steps it would push this kernel past 256 VGPRs.
@@ -251,7 +345,22 @@ bool conv_gemm_8pp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, A
     return p.Kp / PK >= 4;
 }
 
-hipError_t launch_conv_gemm_8pp(const ConvGemmParams& p, Act compute, hipStream_t stream) {
+// per-device tile queues of the DYN variant (9 counters, zeroed once; every launch
+// leaves them zeroed)
+static unsigned* queue_counters() {
+    static unsigned* ctr[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (!ctr[dev]) {
+        void* q = nullptr;
+        if (hipMalloc(&q, 64 * sizeof(unsigned)) != hipSuccess) return nullptr;
+        if (hipMemset(q, 0, 64 * sizeof(unsigned)) != hipSuccess) return nullptr;
+        ctr[dev] = (unsigned*)q;
+    }
+    return ctr[dev];
+}
+
+hipError_t launch_conv_gemm_8pp(const ConvGemmParams& p, Act compute, hipStream_t stream, bool dyn) {
     static const int cus = [] {
         int dev = 0, v = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
@@ -265,14 +374,28 @@ hipError_t launch_conv_gemm_8pp(const ConvGemmParams& p, Act compute, hipStream_
     g = g >= 8 ? g & ~7 : g;
     const dim3 grid(g);
     const bool r = p.R != nullptr;
+    if (dyn) {
+        unsigned* q = queue_counters();
+        if (!q) return hipErrorOutOfMemory;
+        if (g % 8) return hipErrorInvalidValue;  // XCD queues need G/8 workgroups per XCD
+        if (compute == Act::BF16 && r)
+            hipLaunchKernelGGL((conv_gemm_8pp<__bf16, true, true>), grid, dim3(512), 0, stream, p, q);
+        else if (compute == Act::BF16)
+            hipLaunchKernelGGL((conv_gemm_8pp<__bf16, false, true>), grid, dim3(512), 0, stream, p, q);
+        else if (r)
+            hipLaunchKernelGGL((conv_gemm_8pp<_Float16, true, true>), grid, dim3(512), 0, stream, p, q);
+        else
+            hipLaunchKernelGGL((conv_gemm_8pp<_Float16, false, true>), grid, dim3(512), 0, stream, p, q);
+        return hipGetLastError();
+    }
     if (compute == Act::BF16 && r)
-        hipLaunchKernelGGL((conv_gemm_8pp<__bf16, true>), grid, dim3(512), 0, stream, p);
+        hipLaunchKernelGGL((conv_gemm_8pp<__bf16, true>), grid, dim3(512), 0, stream, p, nullptr);
     else if (compute == Act::BF16)
-        hipLaunchKernelGGL((conv_gemm_8pp<__bf16, false>), grid, dim3(512), 0, stream, p);
+        hipLaunchKernelGGL((conv_gemm_8pp<__bf16, false>), grid, dim3(512), 0, stream, p, nullptr);
     else if (r)
-        hipLaunchKernelGGL((conv_gemm_8pp<_Float16, true>), grid, dim3(512), 0, stream, p);
+        hipLaunchKernelGGL((conv_gemm_8pp<_Float16, true>), grid, dim3(512), 0, stream, p, nullptr);
     else
-        hipLaunchKernelGGL((conv_gemm_8pp<_Float16, false>), grid, dim3(512), 0, stream, p);
+        hipLaunchKernelGGL((conv_gemm_8pp<_Float16, false>), grid, dim3(512), 0, stream, p, nullptr);
     return hipGetLastError();
 }
 

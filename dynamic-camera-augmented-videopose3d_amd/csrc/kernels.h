@@ -67,7 +67,7 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
 // Persistent form of the same kernel (conv_gemm_8pp.hip): one workgroup per CU, one
 // continuous LDS-DMA stream across its tiles (K >= 128).
 bool conv_gemm_8pp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
-hipError_t launch_conv_gemm_8pp(const ConvGemmParams& p, Act compute, hipStream_t stream);
+hipError_t launch_conv_gemm_8pp(const ConvGemmParams& p, Act compute, hipStream_t stream, bool dyn = false);
 // measurement only (VP3D_ABL=7 launches): 10 u64 timestamps/ids per workgroup
 hipError_t conv_gemm_8p_set_trace(unsigned long long* buf);
 
