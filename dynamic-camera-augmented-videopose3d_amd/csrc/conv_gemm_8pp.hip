@@ -258,32 +258,42 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8pp(ConvGemmParams p, unsign
 
     int x = 0;
     if constexpr (DYN) {
+        // Tile ids three tiles ahead: the atomic for tile it+3 is issued around tile it's
+        // epilogue (before it without a residual: the stores carry no counted wait, so it
+        // returns under them; after it with one, whose residual waits would otherwise hold
+        // it), published through LDS after K-step 1 of tile it+1 — by then the counted
+        // waits have retired it without stalling — and read after that tile's last K-step.
+        int k_n2 = k_nxt >= 0 && k_cur + 2 * gx < xcnt ? k_cur + 2 * gx : -1;
+        bool pending = false;
+        unsigned fetched = 0;
         while (k_nxt >= 0) {
-            // a tile with a successor: fetch the one after it.  The atomic is issued
-            // here and its value consumed after K-step 1 (by then the counted vmcnt waits
-            // have retired it; it only adds one younger op to them, so they wait a little
-            // more, never less), published through LDS and read after the last K-step.
             int m0, n0;
             tile_k(k_cur, m0, n0);
-            unsigned fetched = 0;
-            if (tid == 0) fetched = atomicAdd(&ctr[xcd], 1u);
             a_rows_k(k_nxt, a_next);
             step(x, W_STREAM{}, true, true, it_cur > 0, m0, n0);
             ++x;
             for (int s = 1; s < nk; ++s, ++x) {
                 step(x, std::integral_constant<int, 6>{}, true, true, false, m0, n0);
-                if (s == 1 && tid == 0) {
-                    s_fetch = 2 * gx + (int)fetched;
+                if (s == 1 && pending && tid == 0) {
+                    s_fetch = 3 * gx + (int)fetched;
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
             }
-            int k_after = __builtin_amdgcn_readfirstlane(s_fetch);  // wave-uniform: SGPR
-            k_after = k_after < xcnt ? k_after : -1;
+            if (pending) {
+                const int kk = __builtin_amdgcn_readfirstlane(s_fetch);  // wave-uniform: SGPR
+                k_n2 = kk < xcnt ? kk : -1;
+                pending = false;
+            }
+            const bool fetch = k_n2 >= 0;  // more tiles may remain on this XCD
+            if (!HAS_R && fetch && tid == 0) fetched = atomicAdd(&ctr[xcd], 1u);
             epilogue_tp<CT, 8, false, HAS_R ? 1 : 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift,
                                                      y_rsrc);
+            if (HAS_R && fetch && tid == 0) fetched = atomicAdd(&ctr[xcd], 1u);
+            pending = fetch;
             zero_acc();
             k_cur = k_nxt;
-            k_nxt = k_after;
+            k_nxt = k_n2;
+            k_n2 = -1;  // tile it+3: read during the next tile when pending
             ++it_cur;
         }
         {
