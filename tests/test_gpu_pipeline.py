@@ -162,6 +162,38 @@ def test_forward_windows_matches_gather_then_forward(dtype, traj):
     assert torch.equal(y, y_ref), (y - y_ref).abs().max().item()
 
 
+@pytest.mark.parametrize("traj", [True, False])
+def test_forward_windows_large_batch(traj):
+    """The bench shape family at 1024 channels: B = 1600 windows puts the expand output
+    (1600 x 81 rows x 2 KB = 265 MB) past the Infinity Cache, so both the gathered and the
+    materialised expand take the nontemporal-store path, the gathered one at 2 row blocks
+    per wave (46-channel input: K = 138) -- still exactly the gather-then-forward output."""
+    from helpers import make_model
+    from vp3d_amd.pipeline import DeviceSequences
+    jin = 23 if traj else 17
+    model, _ = make_model(True, jin=jin, channels=1024)
+    model.cuda()
+    lens = [700, 243, 2000]
+    kps, cams = [], []
+    for i, n in enumerate(lens):
+        kps.append(synth.normalized_windows(21 + i, f"fwl{i}", 1, n)[0])
+        cams.append({"intrinsics": synth.CMU_INTRINSICS,
+                     "extrinsics": synth.camera_extrinsics(6, f"fwl{i}", n)})
+    ds = DeviceSequences(kps, None, cams if traj else None, "cuda")
+    rng = np.random.RandomState(4)
+    B = 1600
+    seq = rng.randint(0, len(lens), size=B)
+    start = np.array([rng.randint(-130, lens[s] + 130) for s in seq])
+    pairs = torch.from_numpy(np.stack([seq, start], -1).astype(np.int32)).cuda()
+    lifter = model.native_lifter(torch.device("cuda", torch.cuda.current_device()))
+    with torch.no_grad():
+        y = lifter.forward_windows(ds, pairs, 243, 121, concat_cams=traj, dtype="bf16")
+        x = ds.gather(pairs, 243, 121, "2d", concat_cams=traj).view(B, 243, jin, 2)
+        y_ref = lifter.forward(x, "bf16")
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref), (y - y_ref).abs().max().item()
+
+
 def test_forward_windows_rejects_feature_mismatch():
     from helpers import make_model
     from vp3d_amd.pipeline import DeviceSequences
