@@ -226,8 +226,8 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
                                                              float scale, float* __restrict__ O) {
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     static_assert(DH == 16 || DH == 32, "head dim");
-    __shared__ float Ks[ATT_WMAX * ATT_LD];
-    __shared__ float Vs[ATT_WMAX * ATT_LD];
+    __shared__ __attribute__((aligned(16))) float Ks[ATT_WMAX * ATT_LD];
+    __shared__ __attribute__((aligned(16))) float Vs[ATT_WMAX * ATT_LD];
     const int w = blockIdx.x, h = blockIdx.y;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t row0 = (int64_t)w * W;
@@ -242,7 +242,10 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
             kv = *(const f32x4*)(r + d);
             vv = *(const f32x4*)(r + 2 * d);
         }
-        *(f32x4*)&Ks[j * ATT_LD + c] = kv;
+        // K columns permuted (c = 4s + g stored at g * DH/4 + s): the QK^T operand of lane
+        // group g is then DH/4 consecutive floats, read with 16-byte LDS reads
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) Ks[j * ATT_LD + e2 * (DH / 4) + c / 4] = kv[e2];
         *(f32x4*)&Vs[j * ATT_LD + c] = vv;
     }
     __syncthreads();
@@ -262,11 +265,17 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const float* __rest
         for (int kb = 0; kb < ATT_WMAX / 16; kb += 2) {
             if (kb < nkb) {
                 f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-                const float* kr = Ks + (kb * 16 + lq) * ATT_LD + g;
+                const float* kr = Ks + (kb * 16 + lq) * ATT_LD + g * NS;
+                f32x4 k0[NS / 4], k1[NS / 4];
+#pragma unroll
+                for (int u = 0; u < NS / 4; ++u) {
+                    k0[u] = *(const f32x4*)(kr + 4 * u);
+                    k1[u] = *(const f32x4*)(kr + 16 * ATT_LD + 4 * u);
+                }
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[4 * s], qf[s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(kr[16 * ATT_LD + 4 * s], qf[s], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(k0[s / 4][s % 4], qf[s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(k1[s / 4][s % 4], qf[s], acc1, 0, 0, 0);
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
