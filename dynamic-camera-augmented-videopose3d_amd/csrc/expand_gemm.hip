@@ -195,7 +195,10 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
                 }
                 const int row = rb * 16 + (lane & 15);
                 const int c16 = nl >> 3;  // 16-byte chunk (8 channels), half (nl >> 2) & 1
-                char* dst = (char*)stage + row * 128 + ((c16 ^ (row & 7)) << 4) + (((nl >> 2) & 1) << 3);
+                // the half is swapped on rows 8-15 of each 16: the 16 lanes of a write group
+                // then cover all 32 banks (rows r and r + 8 otherwise shared them)
+                char* dst = (char*)stage + row * 128 + ((c16 ^ (row & 7)) << 4) +
+                            ((((nl >> 2) & 1) ^ ((row >> 3) & 1)) << 3);
                 *(ct4*)dst = o;
             }
         }
@@ -205,7 +208,8 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
         for (int q = 0; q < 2 * RB; ++q) {
             const int row = q * 8 + (lane >> 3);
             const int c16 = lane & 7;
-            const u32x4 v = stage[row * 8 + (c16 ^ (row & 7))];
+            u32x4 v = stage[row * 8 + (c16 ^ (row & 7))];
+            if (q & 1) v = u32x4{v.z, v.w, v.x, v.y};  // rows 8-15 of 16: halves swapped
             const int m = m_wave + row;
             if (m < p.M) {
                 u32x4* dst = (u32x4*)(Y + (int64_t)m * p.ldy + n0 + c16 * 8);
