@@ -168,6 +168,7 @@ def test_train_dropout_parity_with_oracle(strided, fw, B, T, channels):
     """Dropout p = 0.25: the oracle fed the masks the trainer drew gives the same output,
     loss and gradients; about 75 % of the activations are kept."""
     p = 0.25
+    torch.manual_seed(1234)  # the module draws its dropout seed from torch's generator
     meta = dict(strided=strided, fw=list(fw), causal=False, dense=False, channels=channels)
     from helpers import make_model
     _, sd = make_model(strided, fw, channels=channels, seed=5)
@@ -178,8 +179,11 @@ def test_train_dropout_parity_with_oracle(strided, fw, B, T, channels):
     loss = torch.mean(torch.norm(y - torch.from_numpy(tgt).cuda(), dim=-1))
     loss.backward()
     masks = _masks(m, B, T)
-    keep = np.mean([mk.mean() for mk in masks])
-    assert abs(keep - 0.75) < 0.01, keep
+    # kept fraction over every element of every layer: binomial, 4 sigma (the smallest
+    # case has ~15k elements, sigma 0.35 %; a per-layer mean of means was 1.7 sigma at 1 %)
+    n = sum(mk.size for mk in masks)
+    keep = sum(float(mk.sum()) for mk in masks) / n
+    assert abs(keep - 0.75) < max(0.005, 4 * np.sqrt(0.75 * 0.25 / n)), (keep, n)
 
     rm = _masks(m, B, T, "relu")
     y32, l32, g32, st32 = _oracle(sd, x, tgt, meta, p=p, masks=masks)
