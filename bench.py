@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
 """Headline benchmark: 3D poses/s of the 243-frame-RF, 17-joint, 1024-channel
-TemporalModelOptimized1f lifter on MI355X (BASELINE.json config 2; config 4
-when launched with N > 1 ranks: the window batch is sharded, no collective).
+TemporalModelOptimized1f lifter on MI355X (BASELINE.json configs 2 and 4).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch 65536 | --batch B] [--dtype bf16]
 
-One step = one eval-mode forward of B independent 243-frame windows that are
-already resident in HBM (B poses out).  Every rank processes its own B windows
-(weak scaling); `value` = N*B*K / max-over-ranks(wall time of K steps).
+One step = one eval-mode forward of the global batch of 243-frame windows (65,536 by
+default: config 4), sharded over the N ranks by vp3d_amd.shard.shard_range, every
+rank's shard gathered on device from one seeded window set and resident in HBM before
+the timed region (strong scaling; N = 1 is the single-GPU config-2/4 point).
+`value` = G*K / max-over-ranks(wall time of K steps).  --batch B instead gives every
+rank its own B windows (weak scaling).  At N = 1 the line also carries the fp32
+parity path at the same batch (`fp32`), the config-2 batch sweep {1,024, 8,192,
+65,536} and the CPU baseline.
 
 Besides the JSON contract fields the line carries
   roofline      dominant kernel (block-1 k3 conv GEMM) FLOP per launch / its average
@@ -45,8 +49,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=None, help="windows per GPU per step (8192; 1024 with --train)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--global-batch", type=int, default=65536,
+                    help="windows per step over all ranks (config 4: sharded with shard_range; strong scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="windows per GPU per step instead of --global-batch (weak scaling); the per-step "
+                         "unit count of --train / --sequence / --seq-model")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"],
+                    help="bf16 (configs 2/4), fp16 (--traj, --stream)")
+    ap.add_argument("--sweep", type=lambda v: [int(t) for t in v.split(",") if t], default=[1024, 8192, 65536],
+                    help="config-2 batch sweep on one GPU (windows per step)")
+    ap.add_argument("--no-extras", action="store_true", help="skip the fp32 leg, the sweep and the CPU baseline")
     ap.add_argument("--traj", action="store_true",
                     help="config 3: camera-trajectory conditioned input (46 ch) with the "
                          "on-device window gather inside the timed step")
@@ -63,13 +75,13 @@ def parse():
                     help="sliding-window eval of CoupledTransformer / CoupledLSTM (f32); --batch = poses "
                          "per step (default 16384)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="approximate CPU-baseline sample duration (0 disables)")
+                    help="approximate CPU-baseline duration over its 5 timed runs (0 disables)")
     ap.add_argument("--parity-windows", type=int, default=32)
     ap.add_argument("--settle-seconds", type=float, default=0.5,
                     help="untimed steps after --warmup until the device has run this long")
     args = ap.parse_args()
-    if args.batch is None:
-        args.batch = 1024 if args.train else (16384 if args.seq_model else 65536 if args.sequence else 8192)
+    if args.batch is None and (args.train or args.seq_model or args.sequence):
+        args.batch = 1024 if args.train else (16384 if args.seq_model else 65536)
     return args
 
 
@@ -151,16 +163,9 @@ def stream_main(args, world, rank, dev):
     cpu = None
     if args.cpu_seconds > 0:
         win = xp[:, :RF_FULL].contiguous()
-        lifter_forward(sd, win, FW, causal=True)
-        n, tc = 0, 0.0
-        while tc < args.cpu_seconds:
-            t1 = time.perf_counter()
-            lifter_forward(sd, win, FW, causal=True)
-            tc += time.perf_counter() - t1
-            n += 1
-        cpu = {"value": round(n / tc, 2), "unit": "poses/s", "cores": torch.get_num_threads(),
-               "kind": "port", "sample": f"{n} single-frame causal steps (one 243-frame window "
-                                         f"through the torch-CPU restatement each) in {tc:.1f} s"}
+        cpu = cpu_baseline(lambda: lifter_forward(sd, win, FW, causal=True), 1, "poses/s",
+                           "single-frame causal steps (one 243-frame window through the torch-CPU "
+                           "restatement each, B = 1)", target_s=args.cpu_seconds / 5)
     out = {
         "metric": METRIC, "value": round(world * args.steps / dt, 2), "unit": "poses/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -277,29 +282,16 @@ def train_main(args, world, rank, dev):
         "loss_last": float(loss.item()),
     }
     if args.cpu_seconds > 0:
-        out["cpu_baseline"] = train_cpu_baseline(sd, RF, args.cpu_seconds)
+        from oracle.train_ref import TrainLoop
+        loop = TrainLoop(sd, FW, lr=1e-3, amsgrad=True)
+        rng = np.random.default_rng(0)
+        xb = (rng.standard_normal((8, RF, JOINTS, 2)) * 0.3).astype(np.float32)
+        tb = (rng.standard_normal((8, 1, JOINTS, 3)) * 0.2).astype(np.float32)
+        out["cpu_baseline"] = cpu_baseline(lambda: loop.step(xb, tb), 8, "windows/s",
+                                           "training iterations on batches of 8 windows (dropout 0) through "
+                                           "oracle/train_ref.py (torch-CPU autograd + Adam)",
+                                           target_s=args.cpu_seconds / 5)
     print(json.dumps(out), flush=True)
-
-
-def train_cpu_baseline(sd, RF, seconds):
-    """The oracle's training iteration (reference op sequence, torch-CPU autograd + Adam) on
-    a bounded sample: batches of 8 windows until ~`seconds` elapse."""
-    from oracle.train_ref import TrainLoop
-    threads = torch.get_num_threads()
-    loop = TrainLoop(sd, FW, lr=1e-3, amsgrad=True)
-    rng = np.random.default_rng(0)
-    Bc = 8
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        x = (rng.standard_normal((Bc, RF, JOINTS, 2)) * 0.3).astype(np.float32)
-        tg = (rng.standard_normal((Bc, 1, JOINTS, 3)) * 0.2).astype(np.float32)
-        loop.step(x, tg)
-        n += Bc
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 3), "unit": "windows/s", "cores": threads, "kind": "port",
-            "sample": f"{n} windows (batches of {Bc}, dropout 0) through the oracle's training iteration "
-                      f"(oracle/train_ref.py: torch-CPU autograd + Adam) in {dt:.1f} s"}
 
 
 def seq_flop_per_pose(kind, W=243, d=128, layers=2, ff=128, heads=4, head=(128, 128, 128), cin=46, jout=51,
@@ -384,23 +376,14 @@ def seq_main(args, world, rank, dev):
     }
     if args.cpu_seconds > 0:
         from oracle.seq_lifter_ref import lstm_forward, sliding_windows, transformer_forward
-        threads = torch.get_num_threads()
-        n = 0
-        x2c, xcc = x2.cpu(), xc.cpu()
-        t0 = time.perf_counter()
-        pos = 0
-        while time.perf_counter() - t0 < args.cpu_seconds and pos + 64 <= N:
-            w2, wc = sliding_windows(x2c[:, pos:pos + 64 + W - 1], xcc[:, pos:pos + 64 + W - 1], W)
-            if kind == "transformer":
-                transformer_forward(sd, w2, wc, 4, 2, 3)
-            else:
-                lstm_forward(sd, w2, wc, 128, 2, 3)
-            n += 64
-            pos += 64
-        dtc = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(n / dtc, 2), "unit": "poses/s", "cores": threads, "kind": "port",
-                               "sample": f"{n} sliding windows (batches of 64) through oracle/seq_lifter_ref.py "
-                                         f"(torch-CPU, the reference's op sequence) in {dtc:.1f} s"}
+        w2, wc = sliding_windows(x2[:, :64 + W - 1].cpu(), xc[:, :64 + W - 1].cpu(), W)
+        if kind == "transformer":
+            fn = lambda: transformer_forward(sd, w2, wc, 4, 2, 3)  # noqa: E731
+        else:
+            fn = lambda: lstm_forward(sd, w2, wc, 128, 2, 3)  # noqa: E731
+        out["cpu_baseline"] = cpu_baseline(fn, 64, "poses/s", "64 sliding windows per run through "
+                                           "oracle/seq_lifter_ref.py (torch-CPU, the reference's op sequence)",
+                                           target_s=args.cpu_seconds / 5)
     print(json.dumps(out), flush=True)
 
 
@@ -474,18 +457,288 @@ def sequence_main(args, world, rank, dev):
         "parity": {"frames_checked": P, "max_coord_delta_mm": float(np.abs(got - ref).max()) * 1e3},
     }
     if args.cpu_seconds > 0:
-        nthr = torch.get_num_threads()
         Tc = 2048
         xc = x[:, :Tc + RF - 1].cpu()
-        n, t_cpu = 0, 0.0
-        while t_cpu < args.cpu_seconds:
-            t1 = time.perf_counter()
-            lifter_forward(sd, xc, FW)
-            t_cpu += time.perf_counter() - t1
-            n += Tc
-        out["cpu_baseline"] = {"value": round(n / t_cpu, 2), "unit": "poses/s", "cores": nthr, "kind": "port",
-                               "sample": f"{n} poses as sequences of {Tc + RF - 1} frames through oracle/temporal_ref.py "
-                                         f"(torch-CPU, fp32) in {t_cpu:.1f} s"}
+        out["cpu_baseline"] = cpu_baseline(lambda: lifter_forward(sd, xc, FW), Tc, "poses/s",
+                                           f"one sequence of {Tc + RF - 1} frames -> {Tc} poses per run through "
+                                           "oracle/temporal_ref.py (torch-CPU, fp32)", target_s=args.cpu_seconds / 5)
+    print(json.dumps(out), flush=True)
+
+
+def host_cpu_info():
+    """CPU model and core counts of this host (/proc/cpuinfo)."""
+    model, cores, logical = None, set(), 0
+    try:
+        phys = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    logical += 1
+                elif k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    cores.add((phys, v))
+    except OSError:
+        pass
+    return {"cpu_model": model, "host_physical_cores": len(cores) or None, "host_logical_cpus": logical or None}
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: all physical cores of this host, capped by the CPU share
+    the job was given (OMP_NUM_THREADS: 16 per GPU on the MI355X boxes)."""
+    info = host_cpu_info()
+    n = info["host_physical_cores"] or os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return n, info
+
+
+def cpu_baseline(run_once, units_per_run, unit, sample_desc, repeats=5, target_s=2.5):
+    """Median of `repeats` timed runs (after one warm-up) of the oracle on the host cores.
+    run_once() processes `units_per_run` units; each timed run repeats it to ~target_s."""
+    threads, info = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        t = time.perf_counter()
+        run_once()  # warm-up
+        t1 = max(time.perf_counter() - t, 1e-3)
+        reps = max(1, int(round(target_s / t1)))
+        rates = []
+        for _ in range(repeats):
+            t = time.perf_counter()
+            for _ in range(reps):
+                run_once()
+            rates.append(reps * units_per_run / (time.perf_counter() - t))
+    finally:
+        torch.set_num_threads(prev)
+    rates_sorted = sorted(rates)
+    return {"value": round(float(np.median(rates)), 3), "unit": unit, "cores": threads, "kind": "port",
+            "sample": f"{sample_desc}; median of {repeats} runs of {reps} x {units_per_run} after 1 warm-up "
+                      f"({sum(reps * units_per_run / r for r in rates):.1f} s timed)",
+            "runs": [round(r, 3) for r in rates_sorted], **info,
+            "threads_note": "torch threads = host physical cores capped by the job's CPU share (OMP_NUM_THREADS)"}
+
+
+def timed_steps(step, steps, warmup, settle_s, world):
+    """W warm-up steps, untimed steps until the device has run `settle_s` (clock ramp),
+    then exactly `steps` steps bracketed by barrier + synchronize; returns seconds."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    while time.perf_counter() - t < settle_s:
+        step()
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+LAYER_NAMES = ["expand"] + [f"block{(i // 2) + 1}_{'k3' if i % 2 == 0 else '1x1'}"
+                            for i in range(2 * (len(FW) - 1))] + ["shrink"]
+
+
+def profiled_run(lifter, step, steps, warmup, settle_s, world):
+    """Per-layer times from an untimed pass with events around every launch, then the
+    timed steps with events around the dominant layer only (events on all ten launches
+    cost ~75 us per step).  Returns (dt, per_layer_ms, dominant-layer record)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    while time.perf_counter() - t < settle_s:
+        step()
+        torch.cuda.synchronize()
+    lifter.profile(True)
+    lifter.profile_layers(None)
+    lifter.profile_reset()
+    for _ in range(min(steps, 10)):
+        step()
+    layer_prof = lifter.profile_read()
+    dom_layer = max(layer_prof, key=lambda r: r["ms_total"])["layer"]
+    lifter.profile_layers([dom_layer])
+    lifter.profile_reset()
+    dt = timed_steps(step, steps, 0, 0.0, world)
+    lifter.profile(False)
+    lifter.profile_layers(None)
+    dom = lifter.profile_read()[dom_layer]
+    per_layer = {LAYER_NAMES[r["layer"]]: round(r["ms_total"] / max(r["launches"], 1), 4) for r in layer_prof}
+    return dt, per_layer, dom
+
+
+def roofline_of(dom, peak, traffic=None):
+    avg_ms = max(dom["ms_total"] / max(dom["launches"], 1), 1e-9)
+    achieved = dom["flop"] / (avg_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": f"conv_gemm ({LAYER_NAMES[dom['layer']]})", "achieved": round(achieved, 2),
+            "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+            "avg_launch_ms": round(avg_ms, 4), "launches_timed": dom["launches"], "flop_per_launch": dom["flop"]}
+
+
+def windows_main(args, world, rank, dev):
+    """Configs 2-4: TemporalModelOptimized1f over 243-frame windows resident in HBM.
+
+    Default: a global batch of --global-batch windows (65,536: config 4) sharded over the
+    ranks with vp3d_amd.shard.shard_range (strong scaling; N = 1 is the config-2/4 single-GPU
+    point).  --batch B: B windows per rank (weak scaling).  --traj: config 3, the per-frame
+    K.E + window gather + camera concat inside the step."""
+    from common.models.TemporalModel import TemporalModelOptimized1f
+    from vp3d_amd import synth
+    from vp3d_amd.shard import shard_range
+
+    traj = args.traj
+    dtype = args.dtype or ("fp16" if traj else "bf16")
+    jin = 23 if traj else JOINTS
+    model = TemporalModelOptimized1f(jin, 2, JOINTS, FW, channels=CHANNELS)
+    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model.eval().cuda()
+    RF = model.receptive_field()
+    pad = (RF - 1) // 2
+    from vp3d_amd.pipeline import SyntheticWindowPool
+    pool = SyntheticWindowPool(1000, dev, cameras=traj)
+    if args.batch:
+        G = args.batch * world
+        s, e = rank * args.batch, (rank + 1) * args.batch
+        scaling = "weak"
+    else:
+        G = args.global_batch
+        s, e = shard_range(G, rank, world)
+        scaling = "strong"
+    pairs_all = pool.global_pairs(G)
+    pairs = torch.from_numpy(pairs_all[s:e]).to(dev)
+    B = e - s
+    lifter = model.native_lifter(dev)
+    lifter.reserve(B, RF, dtype)
+    y = torch.empty((B, 1, JOINTS, 3), device=dev)
+    x = None
+    if not traj:
+        # the rank's shard of the global window set, gathered on device and resident
+        x = pool.seqs.gather(pairs, RF, pad, "2d").view(B, RF, jin, 2)
+
+    def make_step(dt_, x_, pairs_, y_):
+        if traj:
+            def step():
+                # config 3: K.E of every frame, then the window gather + camera concat fused
+                # into the expand conv's operand loads, then the stack
+                pool.seqs.refresh_cameras()
+                lifter.forward_windows(pool.seqs, pairs_, RF, pad, concat_cams=True, dtype=dt_, out=y_)
+        else:
+            def step():
+                lifter.forward(x_, dt_, out=y_)
+        return step
+
+    with torch.no_grad():
+        dt, per_layer, dom = profiled_run(lifter, make_step(dtype, x, pairs, y), args.steps, args.warmup,
+                                          args.settle_seconds, world)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = G * args.steps / dt if scaling == "strong" else world * B * args.steps / dt
+    if rank != 0:
+        return
+
+    from oracle.temporal_ref import lifter_forward
+    flop_pose = 358541312 if traj else 352569344
+
+    # ---- parity: the timed kernels' own output on windows from both ends of the shard ----
+    P = min(args.parity_windows, B)
+    idx = torch.cat([torch.arange(P // 2), torch.arange(B - (P - P // 2), B)]).to(dev)
+    xs = pool.seqs.gather(pairs[idx].contiguous(), RF, pad, "2d", concat_cams=traj).view(P, RF, jin, 2)
+    y_fast = y[idx].cpu().numpy()
+    ref = lifter_forward(sd, xs.cpu(), FW, strided=True).numpy()
+    gt = synth.gt_poses(3, "bench_gt", P, JOINTS).reshape(ref.shape)
+
+    def mp(a):
+        return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
+    parity = {"windows": P, "windows_checked": "first and last half of rank 0's shard (timed kernels' output)",
+              "mpjpe_ref_mm": round(mp(ref) * 1e3, 6),
+              "output_rms_m": round(float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))), 6),
+              f"{dtype}_mpjpe_delta_mm": abs(mp(y_fast) - mp(ref)) * 1e3,
+              f"{dtype}_max_coord_delta_mm": float(np.abs(y_fast - ref).max()) * 1e3}
+
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", f"traffic_{dtype}_b{B}{'_traj' if traj else ''}.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": dtype,
+        "data": "synthetic (seeded random-walk 2D keypoint tracks gathered into windows on device, "
+                "counter-hash weights)",
+        "config": {
+            "workload": ("config3 trajectory-conditioned (46ch) " if traj else
+                         ("config4 global batch sharded over ranks, " if scaling == "strong" else "config2 ")
+                         ) + "TemporalModelOptimized1f 243-frame RF windows, 17 joints, 1024 ch",
+            "global_batch": G, "windows_per_gpu": B,
+            "parallelism": f"dp{world} (contiguous shards of one global window set, no collective)"
+            if scaling == "strong" else f"dp{world} (independent windows per rank, no collective)",
+            "flop_per_pose": flop_pose},
+        "tflops_effective": round(value * flop_pose / 1e12, 2),
+        "roofline": roofline_of(dom, PEAK_TFLOPS[dtype], traffic),
+        "per_layer_ms": per_layer,
+        "per_layer_note": "untimed pass with HIP events around every launch",
+        "parity": parity,
+    }
+
+    if world == 1 and not args.no_extras:
+        with torch.no_grad():
+            # ---- fp32 parity path: same windows, same B, fewer steps ----
+            if not traj:
+                y32 = torch.empty_like(y)
+                lifter.reserve(B, RF, "fp32")
+                k32 = max(3, args.steps // 4)
+                dt32, pl32, dom32 = profiled_run(lifter, make_step("fp32", x, pairs, y32), k32, 1, 0.3, 1)
+                v32 = G * k32 / dt32
+                y32s = y32[idx].cpu().numpy()
+                out["fp32"] = {"value": round(v32, 2), "unit": "poses/s", "steps": k32,
+                               "ms_per_step": round(dt32 / k32 * 1e3, 4),
+                               "roofline": roofline_of(dom32, PEAK_TFLOPS["fp32"]),
+                               "per_layer_ms": pl32,
+                               "mpjpe_delta_mm": abs(mp(y32s) - mp(ref)) * 1e3,
+                               "max_coord_delta_mm": float(np.abs(y32s - ref).max()) * 1e3}
+                parity["fp32_mpjpe_delta_mm"] = out["fp32"]["mpjpe_delta_mm"]
+                parity["fp32_max_coord_delta_mm"] = out["fp32"]["max_coord_delta_mm"]
+                # ---- config-2 batch sweep (1 GPU) ----
+                sweep = {}
+                for Bs in args.sweep:
+                    if Bs == B:
+                        sweep[str(Bs)] = round(value, 2)
+                        continue
+                    ps = torch.from_numpy(pool.global_pairs(Bs)).to(dev)
+                    xsw = pool.seqs.gather(ps, RF, pad, "2d").view(Bs, RF, jin, 2)
+                    ysw = torch.empty((Bs, 1, JOINTS, 3), device=dev)
+                    lifter.reserve(Bs, RF, dtype)
+                    ks = max(5, args.steps // 2)
+                    dts = timed_steps(make_step(dtype, xsw, ps, ysw), ks, 3, 0.2, 1)
+                    sweep[str(Bs)] = round(Bs * ks / dts, 2)
+                    del xsw, ysw
+                out["batch_sweep_poses_per_s"] = sweep
+        # ---- CPU baseline: the oracle (reference op sequence) on 64 windows of the same set ----
+        if args.cpu_seconds > 0:
+            xc = pool.seqs.gather(pairs[:64].contiguous(), RF, pad, "2d", concat_cams=traj).view(-1, RF, jin, 2).cpu()
+            cpu = cpu_baseline(lambda: lifter_forward(sd, xc, FW, strided=True), int(xc.shape[0]), "poses/s",
+                               f"windows of 243x{jin}x2 through oracle/temporal_ref.py (torch-CPU, fp32, batch "
+                               f"{int(xc.shape[0])})", target_s=args.cpu_seconds / 5)
+            out["cpu_baseline"] = cpu
+            out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+            if "fp32" in out:
+                out["fp32"]["speedup_vs_cpu"] = round(out["fp32"]["value"] / cpu["value"], 1)
     print(json.dumps(out), flush=True)
 
 
@@ -510,202 +763,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if args.stream or args.train or args.seq_model or args.sequence:
+        if args.dtype is None:
+            args.dtype = "fp16" if args.stream else "bf16"
         fn = (train_main if args.train else seq_main if args.seq_model else
               sequence_main if args.sequence else stream_main)
         fn(args, world, rank, dev)
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-
-    from common.models.TemporalModel import TemporalModelOptimized1f
-    from vp3d_amd import synth
-
-    jin = 23 if args.traj else JOINTS
-    model = TemporalModelOptimized1f(jin, 2, JOINTS, FW, channels=CHANNELS)
-    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    model.eval().cuda()
-    model.set_compute_dtype(args.dtype)
-    RF = model.receptive_field()
-    B = args.batch
-
-    pipe = None
-    if args.traj:
-        from vp3d_amd.pipeline import SyntheticTrajectoryBatcher
-        pipe = SyntheticTrajectoryBatcher(B, RF, seed=1000 + rank, device=dev)
-        x = None
     else:
-        x = synth_windows(B, RF, jin, 1000 + rank, dev)
-    lifter = model.native_lifter(dev)
-    lifter.reserve(B, RF, args.dtype)
-    y = torch.empty((B, 1, JOINTS, 3), device=dev)
-
-    last_in = [x]
-
-    def step():
-        if pipe is not None:
-            # config 3: K.E of every frame + window gather + camera concat + forward,
-            # the gather fused into the expand conv's operand loads
-            pairs = pipe.next_pairs()
-            lifter.forward_windows(pipe.seqs, pairs, RF, pipe.pad, concat_cams=True, dtype=args.dtype,
-                                   out=y)
-            last_in[0] = pairs
-        else:
-            lifter.forward(x, args.dtype, out=y)
-
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step()
-        # then untimed steps until the device has been busy for ~0.5 s: after a cold
-        # start (the trajectory setup leaves the GPU idle for seconds) the step period
-        # falls from ~5.8 to ~3.2 ms over the first ~20 steps as the clocks ramp
-        # (profiles/r01f_traj_step_ramp.txt), which a 5-step warm-up does not cover
-        torch.cuda.synchronize()
-        t_settle = time.perf_counter()
-        while time.perf_counter() - t_settle < args.settle_seconds:
-            step()
-            torch.cuda.synchronize()
-        # per-layer times from an untimed pass with events around every launch; the timed
-        # loop below carries events around the dominant layer only (events on all ten
-        # launches cost ~75 us per step)
-        lifter.profile(True)
-        lifter.profile_layers(None)
-        lifter.profile_reset()
-        for _ in range(min(args.steps, 10)):
-            step()
-        layer_prof = lifter.profile_read()
-        dom_layer = max(layer_prof, key=lambda r: r["ms_total"])["layer"]
-        lifter.profile_layers([dom_layer])
-        lifter.profile_reset()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        dt = time.perf_counter() - t0
-        lifter.profile(False)
-        lifter.profile_layers(None)
-    prof = lifter.profile_read()
-
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
-    total_poses = world * B * args.steps
-    value = total_poses / dt
-    # dominant kernel: its HIP-event duration over the timed steps
-    dom = prof[dom_layer]
-    dom_avg_ms = max(dom["ms_total"] / max(dom["launches"], 1), 1e-9)
-    achieved = dom["flop"] / (dom_avg_ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[args.dtype]
-    layer_names = ["expand"] + [f"block{(i // 2) + 1}_{'k3' if i % 2 == 0 else '1x1'}"
-                                for i in range(2 * (len(FW) - 1))] + ["shrink"]
-    per_layer = {layer_names[r["layer"]]: round(r["ms_total"] / max(r["launches"], 1), 4)
-                 for r in layer_prof}
-
-    out = None
-    if rank == 0:
-        # ---- parity on a window subset (oracle = reference op sequence on CPU) ----
-        from oracle.temporal_ref import lifter_forward
-        # the timed kernels' own output (last timed step, full batch B) on the first
-        # P windows, plus the fp32 parity path on the same windows
-        P = min(args.parity_windows, B)
-        idx = torch.cat([torch.arange(P // 2), torch.arange(B - (P - P // 2), B)]).to(dev)
-        xfull = pipe.gather(last_in[0]) if pipe is not None else last_in[0]
-        xs = xfull[idx].contiguous()
-        y_fast = y[idx].cpu().numpy()
-        with torch.no_grad():
-            model.set_compute_dtype("fp32")
-            y_32 = model(xs).cpu().numpy()
-            model.set_compute_dtype(args.dtype)
-        ref = lifter_forward(sd, xs.cpu(), FW, strided=True).numpy()
-        gt = synth.gt_poses(3, "bench_gt", P, JOINTS).reshape(ref.shape)
-
-        def mp(a):
-            return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
-        parity = {
-            "windows": P,
-            "windows_checked": "first and last half of the timed batch (timed kernels' output)",
-            "mpjpe_ref_mm": round(mp(ref) * 1e3, 6),
-            "fp32_mpjpe_delta_mm": abs(mp(y_32) - mp(ref)) * 1e3,
-            "fp32_max_coord_delta_mm": float(np.abs(y_32 - ref).max()) * 1e3,
-            f"{args.dtype}_mpjpe_delta_mm": abs(mp(y_fast) - mp(ref)) * 1e3,
-            f"{args.dtype}_max_coord_delta_mm": float(np.abs(y_fast - ref).max()) * 1e3,
-        }
-
-        # ---- CPU baseline: the oracle on a bounded sample of the same workload ----
-        cpu = None
-        if args.cpu_seconds > 0:
-            nthr = torch.get_num_threads()
-            cb = 64
-            xc = xs[:1].cpu().expand(cb, -1, -1, -1).contiguous()
-            lifter_forward(sd, xc[:8], FW, strided=True)  # warm-up
-            n, t_cpu = 0, 0.0
-            while t_cpu < args.cpu_seconds:
-                t1 = time.perf_counter()
-                lifter_forward(sd, xc, FW, strided=True)
-                t_cpu += time.perf_counter() - t1
-                n += cb
-            cpu = {"value": round(n / t_cpu, 2), "unit": "poses/s", "cores": nthr, "kind": "port",
-                   "sample": f"{n} windows of 243x17x2 through the torch-CPU restatement "
-                             f"(oracle/temporal_ref.py, fp32, batch {cb}) in {t_cpu:.1f} s"}
-
-        traffic = None
-        tfile = os.path.join(REPO, "profiles", f"traffic_{args.dtype}_b{B}.json")
-        if os.path.exists(tfile):
-            with open(tfile) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-
-        flop_pose = 358541312 if args.traj else 352569344
-        out = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "poses/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.dtype,
-            "data": "synthetic (seeded random-walk 2D windows, counter-hash weights)",
-            "config": {
-                "workload": ("config3 trajectory-conditioned (46ch) " if args.traj else "config2 ")
-                            + "TemporalModelOptimized1f 243-frame RF windows, 17 joints, 1024 ch",
-                "windows_per_gpu": B,
-                "global_batch": B * world,
-                "parallelism": f"dp{world} (independent window shards, no collective)",
-                "flop_per_pose": flop_pose,
-            },
-            "tflops_effective": round(value * flop_pose / 1e12, 2),
-            "roofline": {
-                "bound": "mfma",
-                "kernel": f"conv_gemm ({layer_names[dom['layer']]})",
-                "achieved": round(achieved, 2),
-                "peak": peak,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4),
-                "traffic": traffic,
-                "avg_launch_ms": round(dom_avg_ms, 4),
-                "launches_timed": dom["launches"],
-                "flop_per_launch": dom["flop"],
-            },
-            "per_layer_ms": per_layer,
-            "per_layer_note": "untimed pass with HIP events around every launch",
-            "cpu_baseline": cpu,
-            "parity": parity,
-        }
-        if cpu:
-            out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
-        print(json.dumps(out), flush=True)
+        windows_main(args, world, rank, dev)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -315,35 +315,25 @@ hipError_t launch_f32(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t
     return hipGetLastError();
 }
 
-// Which 256x256 kernel a large layer runs on (VP3D_GEMM overrides for A/B runs):
+// Which 256x256 kernel a large layer runs on:
 //   default: the ping-pong kernel (conv_gemm_8p.hip) for contiguous-tap layers (the
 //   strided k-tap convs: 1.20 vs 1.22 ms on block 1 at B = 8192; the 1x1 convs with a
-//   residual: 0.54 vs 0.59 ms), the LDS-ring kernel (conv_gemm_big.hip) for dilated convs;
-//   VP3D_GEMM=8p -> 8p everywhere; 8pp -> its persistent form (4-7 % slower: a static
-//   tile assignment loses the hardware dispatcher's balancing across CUs whose clocks
-//   differ); big / persist / pp / tp -> that schedule everywhere.
+//   residual: 0.54 vs 0.59 ms), the LDS-ring kernel (conv_gemm_big.hip) for dilated convs
+//   (taps gathered from rows d apart; sequence mode, 65,536 frames: 0.39-0.40 vs 0.42 ms).
+//   VP3D_GEMM=8p -> 8p wherever eligible, VP3D_GEMM=big -> the LDS-ring kernel everywhere
+//   (both kernels are on the default path, so both forms are parity-tested).  The round-1
+//   A/B schedules (persistent, dynamic-queue, older ping-pong, transposed persistent) were
+//   3-10 % slower and now live outside the library, in tools/ubench/retired/.
+//   Read at every launch (a getenv per layer is noise next to the kernel), so a test can
+//   flip it within one process.
 int gemm_8p_mode() {
-    static const int v = [] {
-        const char* e = getenv("VP3D_GEMM");
-        if (!e) return 1;
-        if (strcmp(e, "8pp") == 0) return 3;
-        if (strcmp(e, "8pd") == 0) return 4;
-        return strcmp(e, "8p") == 0 ? 2 : 0;
-    }();
-    return v;
+    const char* e = getenv("VP3D_GEMM");
+    if (!e) return 1;
+    if (strcmp(e, "8p") == 0) return 2;
+    return strcmp(e, "big") == 0 ? 0 : 1;
 }
-// VP3D_GEMM=8pp: the persistent ping-pong kernel (conv_gemm_8pp.hip) wherever 8p runs
-bool gemm_8pp_env() { return gemm_8p_mode() == 3 || gemm_8p_mode() == 4; }
-// VP3D_GEMM=8pd: the persistent kernel with per-XCD dynamic tile queues
-bool gemm_8pd_env() { return gemm_8p_mode() == 4; }
 bool gemm_8p_env(const ConvGemmParams& p) {
     const int m = gemm_8p_mode();
-    if (m == 3 || m == 4) return true;
-    // default: the ping-pong kernel for contiguous-tap convs (the strided k3 convs and,
-    // since its residual preload stopped spilling, the 1x1 convs with a residual: block 1
-    // at B = 8192 0.54 vs 0.59 ms on the LDS-ring kernel); the dilated k3 convs (taps
-    // gathered from rows d apart) run faster on the LDS-ring kernel (sequence mode, 65,536
-    // frames: 0.39-0.40 vs 0.42 ms per layer)
     return m == 2 || (m == 1 && p.dil == 1);
 }
 
@@ -452,19 +442,10 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
             hipLaunchKernelGGL(conv_gemm_narrow<f16>, g, dim3(256), 0, stream, p);
         return hipGetLastError();
     }
-    if (conv_gemm_tp_eligible(p, a_type, out_type, compute)) return launch_conv_gemm_tp(p, compute, stream);
     if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
-        conv_gemm_8p_eligible(p, a_type, out_type, compute)) {
-        if (gemm_8pp_env() && conv_gemm_8pp_eligible(p, a_type, out_type, compute))
-            return launch_conv_gemm_8pp(p, compute, stream, gemm_8pd_env());
+        conv_gemm_8p_eligible(p, a_type, out_type, compute))
         return launch_conv_gemm_8p(p, compute, stream);
-    }
-    if (conv_gemm_big_eligible(p, a_type, out_type, compute))
-        switch (big_schedule()) {
-            case 1: return launch_conv_gemm_persist(p, out_type, compute, stream);
-            case 2: return launch_conv_gemm_pp(p, out_type, compute, stream);
-            default: return launch_conv_gemm_big(p, out_type, compute, stream);
-        }
+    if (conv_gemm_big_eligible(p, a_type, out_type, compute)) return launch_conv_gemm_big(p, out_type, compute, stream);
     const int aes = a_type == Act::F32 ? 4 : 2;
     int amode = A_SCALAR;
     if ((p.Ktap % kH16Bk == 0) && (p.lda % 8 == 0) && aligned(p.A, 16))

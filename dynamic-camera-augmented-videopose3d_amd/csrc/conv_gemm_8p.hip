@@ -64,7 +64,7 @@ __device__ __forceinline__ void trace_stamp(int wg, int slot) {
     if (!g_trace) return;
     g_trace[(size_t)wg * 10 + slot] = rt;
 }
-template <typename CT, int ABL = 0, bool NT = false>
+template <typename CT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[PRING + 2 * PMAXN * 4];
     float* const s_scale = (float*)(smem + PRING);
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_8p(ConvGemmParams p) {
     if (ABL == 7 && tid == 0) trace_stamp(blockIdx.x, 2);
 
     const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.ldy * sizeof(CT)));
-    epilogue_tp<CT, 8, true, -1, NT ? 2 : 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc, res);
+    epilogue_tp<CT, 8, true, -1, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc, res);
     if (ABL == 7) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -247,35 +247,28 @@ bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
     return true;
 }
 
-// VP3D_GEMM_NT=1: nontemporal output stores on every layer, 2: on outputs larger than
-// the 256 MB Infinity Cache only (A/B)
-static bool gemm_nt(const ConvGemmParams& p) {
-    static const int v = [] {
-        const char* e = getenv("VP3D_GEMM_NT");
-        return e ? atoi(e) : 0;
-    }();
-    return v == 1 || (v == 2 && (int64_t)p.M * p.ldy * 2 > ((int64_t)256 << 20));
-}
-
 hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream) {
     const dim3 grid(((p.M + PM - 1) / PM) * (p.N / PN));
+#ifdef VP3D_ABLATION
+    // measurement builds only (tools/ubench/gemm_check): VP3D_ABL selects an ablated loop
     static const int abl = [] {
         const char* e = getenv("VP3D_ABL");
         return e ? atoi(e) : 0;
     }();
-    if (compute == Act::BF16 && abl == 1)
-        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 1>), grid, dim3(512), 0, stream, p);
-    else if (compute == Act::BF16 && abl == 2)
-        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 2>), grid, dim3(512), 0, stream, p);
-    else if (compute == Act::BF16 && abl == 3)
-        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 3>), grid, dim3(512), 0, stream, p);
-    else if (compute == Act::BF16 && abl == 4)
-        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 4>), grid, dim3(512), 0, stream, p);
-    else if (compute == Act::BF16 && abl == 7)
-        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 7>), grid, dim3(512), 0, stream, p);
-    else if (compute == Act::BF16 && gemm_nt(p))
-        hipLaunchKernelGGL((conv_gemm_8p<__bf16, 0, true>), grid, dim3(512), 0, stream, p);
-    else if (compute == Act::BF16)
+    if (compute == Act::BF16 && abl != 0) {
+        switch (abl) {
+            case 1: hipLaunchKernelGGL((conv_gemm_8p<__bf16, 1>), grid, dim3(512), 0, stream, p); break;
+            case 2: hipLaunchKernelGGL((conv_gemm_8p<__bf16, 2>), grid, dim3(512), 0, stream, p); break;
+            case 3: hipLaunchKernelGGL((conv_gemm_8p<__bf16, 3>), grid, dim3(512), 0, stream, p); break;
+            case 4: hipLaunchKernelGGL((conv_gemm_8p<__bf16, 4>), grid, dim3(512), 0, stream, p); break;
+            default: hipLaunchKernelGGL((conv_gemm_8p<__bf16, 7>), grid, dim3(512), 0, stream, p);
+        }
+        return hipGetLastError();
+    }
+#endif
+    // (nontemporal output stores, VP3D_GEMM_NT in round 1, measured slower on every layer:
+    // b4 k3 0.072 -> 0.083 ms, b1 k3 1.22 -> 1.25-1.29 ms)
+    if (compute == Act::BF16)
         hipLaunchKernelGGL((conv_gemm_8p<__bf16>), grid, dim3(512), 0, stream, p);
     else
         hipLaunchKernelGGL((conv_gemm_8p<_Float16>), grid, dim3(512), 0, stream, p);

@@ -66,39 +66,26 @@ __device__ __forceinline__ void wait_vm(int after) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// Scheduling pattern of one pipelined K-step (sched_group_barrier needs literal
-// arguments, hence the template recursion): group g = 4 MFMAs, then 2 (g < 4) or 1
-// fragment reads of the next step, then one LDS-DMA piece while g < DMA.
-template <int DMA, int G = 0>
-__device__ __forceinline__ void sched_step_pattern() {
-    if constexpr (G < 8) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, G < 4 ? 2 : 1, 0);
-        if constexpr (G < DMA) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        sched_step_pattern<DMA, G + 1>();
-    }
-}
-
 __device__ __forceinline__ void block_sync_lds() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
 
-// PIPE:   fragments of K-step s+1 are read from LDS into a second register set
-//         while the MFMAs of step s run (the ds_read latency leaves the critical path);
-// PRIO:   s_setprio(1) around each MFMA cluster (cdna_hip_programming.md §5.5 T5);
-// SPREAD: (with PIPE) the LDS-DMA pieces of the refill are issued one per MFMA row
-//         group instead of back to back after the barrier.
-template <typename CT, typename OT, int NW_N, int NSLOT, bool PIPE, bool PRIO, bool SPREAD = false,
-          bool PIN = false>
-__global__ __launch_bounds__(128 * NW_N, 2) void conv_gemm_h16_big(ConvGemmParams p) {
-    using C = BigCfg<NW_N, NSLOT>;
+// Main loop (one schedule; round 1 measured plain / prio / spread variants at
+// 1010-1130 TFLOP/s vs 1138 for this one on the block-1 k3 layer): the fragments of
+// K-step s+1 are read from LDS into a second register set while the MFMAs of step s
+// run, and the program order is pinned with sched_barrier: per group g of 4 MFMAs
+// (A row g), two (g < 6) fragment reads of the next step and one LDS-DMA refill piece.
+template <typename CT, typename OT>
+__global__ __launch_bounds__(512, 2) void conv_gemm_h16_big(ConvGemmParams p) {
+    using C = BigCfg<4, 4>;
+    constexpr int NSLOT = 4;
     __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
-    const int wr = wid / NW_N, wc = wid % NW_N;
+    const int wr = wid / 4, wc = wid % 4;
 
     const int ntn = (p.N + C::BN - 1) / C::BN;
     const int ntm = (p.M + BM2 - 1) / BM2;
@@ -147,22 +134,8 @@ __global__ __launch_bounds__(128 * NW_N, 2) void conv_gemm_h16_big(ConvGemmParam
         }
     };
     auto issue = [&](int s) {
-        const int k0 = s * BK2;
-        const int tap = k0 / p.Ktap;
-        const int cin = k0 - tap * p.Ktap + dma_c * 8;
-        char* slot = smem + (s % NSLOT) * C::SLOT_BYTES;
 #pragma unroll
-        for (int q = 0; q < C::A_PIECES; ++q) {
-            const CT* ga = A + (int64_t)(a_src[q] + tap * p.dil) * p.lda + cin;
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)ga,
-                                             (lds_ptr_t)(slot + (wid + C::NWAVES * q) * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < C::B_PIECES; ++q) {
-            const CT* gb = W + b_off[q] + k0;
-            __builtin_amdgcn_global_load_lds(
-                (gbl_ptr_t)gb, (lds_ptr_t)(slot + BM2 * BK2 * 2 + (wid + C::NWAVES * q) * 1024), 16, 0, 0);
-        }
+        for (int idx = 0; idx < C::DMA_PER_STEP; ++idx) issue_piece(s, idx);
     };
 
     // ---- fragment reads: row (l & 15) of each 16-row block, logical chunk (l >> 4)
@@ -189,106 +162,62 @@ __global__ __launch_bounds__(128 * NW_N, 2) void conv_gemm_h16_big(ConvGemmParam
         for (int i = 0; i < 8; ++i) f.a[i] = *(const u32x4*)(slot + a_frag_off + i * 16 * 64);
     };
     auto mma = [&](const Frag& f) {
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<CT>(f.a[i], f.b[j], acc[i][j]);
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     };
 
     const int nk = p.Kp / BK2;
     const int pre = nk < NSLOT - 1 ? nk : NSLOT - 1;
     for (int s = 0; s < pre; ++s) issue(s);
 
-    if constexpr (!PIPE) {
-        for (int s = 0; s < nk; ++s) {
-            const int left = nk - 1 - s;
-            wait_vm<C::DMA_PER_STEP>(left < NSLOT - 2 ? left : NSLOT - 2);
-            block_sync_lds();  // slot s landed for every wave; slot s-1 fully consumed
-            if (s + NSLOT - 1 < nk) issue(s + NSLOT - 1);
-            Frag f;
-            read_frags(s, f);
-            mma(f);
-        }
-    } else {
-        // stage s+1 must be resident one step early; slot s-1 (read during step s-2,
-        // consumed by step s-1) is the one refilled at step s
-        wait_vm<C::DMA_PER_STEP>(pre - 1);
+    // stage s+1 must be resident one step early; slot s-1 (read during step s-2,
+    // consumed by step s-1) is the one refilled at step s
+    wait_vm<C::DMA_PER_STEP>(pre - 1);
+    block_sync_lds();
+    Frag f0, f1;
+    read_frags(0, f0);
+    // steady state: compile-time wait counts, no branches between the reads and the MFMAs
+    auto step_full = [&](int s, Frag& cur, Frag& nxt) {
+        wait_vm<C::DMA_PER_STEP>(NSLOT - 3);
         block_sync_lds();
-        Frag f0, f1;
-        read_frags(0, f0);
-        auto mma_refill = [&](const Frag& cur, int s_refill) {
-            if constexpr (SPREAD) {
+        const char* slot = smem + ((s + 1) % NSLOT) * C::SLOT_BYTES;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
+        for (int g = 0; g < 8; ++g) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<CT>(cur.a[i], cur.b[j], acc[i][j]);
-                    if (i < C::DMA_PER_STEP) issue_piece(s_refill, i);
-                }
-            } else {
-                issue(s_refill);
-                mma(cur);
+            for (int j = 0; j < 4; ++j) acc[g][j] = mfma16<CT>(cur.a[g], cur.b[j], acc[g][j]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (g < 2) {
+                nxt.b[2 * g] = *(const u32x4*)(slot + b_frag_off + (2 * g) * 16 * 64);
+                nxt.b[2 * g + 1] = *(const u32x4*)(slot + b_frag_off + (2 * g + 1) * 16 * 64);
+            } else if (g < 6) {
+                nxt.a[2 * (g - 2)] = *(const u32x4*)(slot + a_frag_off + (2 * (g - 2)) * 16 * 64);
+                nxt.a[2 * (g - 2) + 1] = *(const u32x4*)(slot + a_frag_off + (2 * (g - 2) + 1) * 16 * 64);
             }
-        };
-        // steady state: every step refills a slot and prefetches the next fragments,
-        // with compile-time wait counts and no branches between the reads and the MFMAs
-        // PIN: program order = issue order, fenced with sched_barrier: per group g of
-        // 4 MFMAs (A row g), the next step's fragment reads (B first) and one DMA piece
-        auto step_pinned = [&](int s, Frag& cur, Frag& nxt) {
-            wait_vm<C::DMA_PER_STEP>(NSLOT - 3);
-            block_sync_lds();
-            const char* slot = smem + ((s + 1) % NSLOT) * C::SLOT_BYTES;
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[g][j] = mfma16<CT>(cur.a[g], cur.b[j], acc[g][j]);
-                __builtin_amdgcn_sched_barrier(0);
-                if (g < 2) {
-                    nxt.b[2 * g] = *(const u32x4*)(slot + b_frag_off + (2 * g) * 16 * 64);
-                    nxt.b[2 * g + 1] = *(const u32x4*)(slot + b_frag_off + (2 * g + 1) * 16 * 64);
-                } else if (g < 6) {
-                    nxt.a[2 * (g - 2)] = *(const u32x4*)(slot + a_frag_off + (2 * (g - 2)) * 16 * 64);
-                    nxt.a[2 * (g - 2) + 1] = *(const u32x4*)(slot + a_frag_off + (2 * (g - 2) + 1) * 16 * 64);
-                }
-                if (g < C::DMA_PER_STEP) issue_piece(s + NSLOT - 1, g);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        };
-        auto step_full = [&](int s, Frag& cur, Frag& nxt) {
-            if constexpr (PIN) {
-                step_pinned(s, cur, nxt);
-                return;
-            }
-            wait_vm<C::DMA_PER_STEP>(NSLOT - 3);
-            block_sync_lds();
-            read_frags(s + 1, nxt);
-            mma_refill(cur, s + NSLOT - 1);
-            // pin the schedule: the MFMAs of step s in 8 groups of 4, the 12 fragment
-            // reads of step s+1 and the LDS-DMA refill pieces spread between them (so
-            // neither the reads nor the DMA issue stall the matrix pipe)
-            sched_step_pattern<C::DMA_PER_STEP>();
-        };
-        int s = 0;
-        for (; s + NSLOT < nk; s += 2) {
-            step_full(s, f0, f1);
-            step_full(s + 1, f1, f0);
+            if (g < C::DMA_PER_STEP) issue_piece(s + NSLOT - 1, g);
+            __builtin_amdgcn_sched_barrier(0);
         }
-        // tail: the last few steps (no refills, runtime wait counts)
-        auto step_tail = [&](int s2, Frag& cur, Frag& nxt) {
-            if (s2 + 1 < nk) {
-                const int issued = nk < s2 + NSLOT - 1 ? nk : s2 + NSLOT - 1;
-                wait_vm<C::DMA_PER_STEP>(issued - (s2 + 2));
-                block_sync_lds();
-                if (s2 + NSLOT - 1 < nk) issue(s2 + NSLOT - 1);
-            }
-            read_frags(s2 + 1, nxt);  // past the last step this reads a stale slot, unused
-            mma(cur);
-        };
-        for (; s < nk; s += 2) {
-            step_tail(s, f0, f1);
-            if (s + 1 < nk) step_tail(s + 1, f1, f0);
+    };
+    int s = 0;
+    for (; s + NSLOT < nk; s += 2) {
+        step_full(s, f0, f1);
+        step_full(s + 1, f1, f0);
+    }
+    // tail: the last few steps (no refills, runtime wait counts)
+    auto step_tail = [&](int s2, Frag& cur, Frag& nxt) {
+        if (s2 + 1 < nk) {
+            const int issued = nk < s2 + NSLOT - 1 ? nk : s2 + NSLOT - 1;
+            wait_vm<C::DMA_PER_STEP>(issued - (s2 + 2));
+            block_sync_lds();
+            if (s2 + NSLOT - 1 < nk) issue(s2 + NSLOT - 1);
         }
+        read_frags(s2 + 1, nxt);  // past the last step this reads a stale slot, unused
+        mma(cur);
+    };
+    for (; s < nk; s += 2) {
+        step_tail(s, f0, f1);
+        if (s + 1 < nk) step_tail(s + 1, f1, f0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -297,55 +226,7 @@ __global__ __launch_bounds__(128 * NW_N, 2) void conv_gemm_h16_big(ConvGemmParam
     epilogue_vec<OT, 8, 32>(p, acc, (float*)smem + wid * 32 * kEpiLd, mw, nw, lane);
 }
 
-// Tile shape choice (VP3D_BIG_TILE=256|128 overrides, for A/B runs):
-//   256x256, 8 waves, 4-slot ring (128 KB LDS): one workgroup per CU, least L2 traffic
-//   256x128, 4 waves, 3-slot ring (72 KB LDS): two workgroups per CU, so one
-//   workgroup's prologue/epilogue overlaps the other's MFMA main loop
-// Main-loop variant (VP3D_BIG_VARIANT=plain|pipe|pipe_prio|pipe_spread|pipe_pinned,
-// default pipe_pinned: 1138 TFLOP/s on the block-1 k3 layer vs 1010 for plain).
-int big_variant() {
-    static int v = [] {
-        const char* e = getenv("VP3D_BIG_VARIANT");
-        if (!e) return 4;
-        if (!strcmp(e, "plain")) return 0;
-        if (!strcmp(e, "pipe_prio")) return 2;
-        if (!strcmp(e, "pipe_spread")) return 3;
-        if (!strcmp(e, "pipe_pinned")) return 4;
-        return 1;
-    }();
-    return v;
-}
-
-// Ring depth of the 256x256 tile (VP3D_BIG_SLOTS=4|5, default 4: measured faster than
-// 5, which uses all 160 KiB of LDS).
-int big_slots() {
-    static int v = [] {
-        const char* e = getenv("VP3D_BIG_SLOTS");
-        return (e && atoi(e) == 5) ? 5 : 4;
-    }();
-    return v;
-}
-
-int big_tile_n() {
-    static int v = [] {
-        const char* e = getenv("VP3D_BIG_TILE");
-        return (e && atoi(e) == 128) ? 128 : 256;
-    }();
-    return v;
-}
-
 }  // namespace
-
-int big_schedule() {
-    static int v = [] {
-        const char* e = getenv("VP3D_GEMM");
-        if (big_tile_n() != 256 || !e) return 0;
-        if (!strcmp(e, "persist")) return 1;
-        if (!strcmp(e, "pp")) return 2;
-        return 0;
-    }();
-    return v;
-}
 
 bool conv_gemm_big_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
     if (compute == Act::F32 || a_type != compute) return false;
@@ -355,50 +236,16 @@ bool conv_gemm_big_eligible(const ConvGemmParams& p, Act a_type, Act out_type, A
     if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
         (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
         return false;
-    // enough tiles to fill the 256 CUs several times over
-    const int bn = big_tile_n();
-    const int64_t tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + bn - 1) / bn);
     // enough tiles to fill the 256 CUs (block 3 of the 1f model at B = 8192: 384 tiles,
     // 1.5 rounds, still ahead of the 128x128 kernel: 0.17 vs 0.21 ms)
-    const char* th = getenv("VP3D_BIG_MIN_TILES");
-    return tiles >= (th ? atoi(th) : (bn == 256 ? 384 : 768));
-}
-
-template <typename CT, typename OT, int NW_N, int NSLOT>
-void launch_big_v(const ConvGemmParams& p, dim3 grid, hipStream_t stream) {
-    switch (big_variant()) {
-        case 0:
-            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, false, false>), grid,
-                               dim3(128 * NW_N), 0, stream, p);
-            break;
-        case 2:
-            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, true, true>), grid,
-                               dim3(128 * NW_N), 0, stream, p);
-            break;
-        case 3:
-            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, true, false, true>), grid,
-                               dim3(128 * NW_N), 0, stream, p);
-            break;
-        case 4:
-            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, true, false, true, true>), grid,
-                               dim3(128 * NW_N), 0, stream, p);
-            break;
-        default:
-            hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT, NW_N, NSLOT, true, false>), grid,
-                               dim3(128 * NW_N), 0, stream, p);
-    }
+    const int64_t tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + 255) / 256);
+    return tiles >= 384;
 }
 
 template <typename CT, typename OT>
 hipError_t launch_big_t(const ConvGemmParams& p, hipStream_t stream) {
-    if (big_tile_n() == 256) {
-        const dim3 g(((p.M + BM2 - 1) / BM2) * ((p.N + 255) / 256));
-        if (big_slots() == 5)
-            launch_big_v<CT, OT, 4, 5>(p, g, stream);
-        else
-            launch_big_v<CT, OT, 4, 4>(p, g, stream);
-    } else
-        launch_big_v<CT, OT, 2, 3>(p, dim3(((p.M + BM2 - 1) / BM2) * ((p.N + 127) / 128)), stream);
+    const dim3 g(((p.M + BM2 - 1) / BM2) * ((p.N + 255) / 256));
+    hipLaunchKernelGGL((conv_gemm_h16_big<CT, OT>), g, dim3(512), 0, stream, p);
     return hipGetLastError();
 }
 

@@ -224,19 +224,6 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
     }
 }
 
-// Output stores: nontemporal (nt) by default when the output exceeds the 256 MB Infinity
-// Cache; VP3D_EXPAND_NT=0 for default-policy stores.
-// The 1.36 GB output (B = 8192) cannot stay in the 256 MB Infinity Cache anyway; streamed
-// past it, it leaves the caches to the weights and the block-1 conv that follows runs
-// 1-1.5 % faster (3.10-3.12 vs 3.14-3.18 ms per step, A/B on one box).
-bool expand_nt() {
-    static const bool v = [] {
-        const char* e = getenv("VP3D_EXPAND_NT");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
-}
-
 template <typename CT, int RB, bool GATHER, bool NT>
 hipError_t launch_rb_nt(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     const dim3 grid((p.M + 64 * RB - 1) / (64 * RB));
@@ -251,40 +238,25 @@ hipError_t launch_rb_nt(const ConvGemmParams& p, const GatherSrc& g, int nks, hi
     return hipGetLastError();
 }
 
-template <typename CT, int RB, bool GATHER>
-hipError_t launch_rb(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
-    // only outputs larger than the Infinity Cache; a smaller one is better left cached for
-    // the next layer
-    const bool nt = expand_nt() && (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
-    return nt ? launch_rb_nt<CT, RB, GATHER, true>(p, g, nks, s)
-                       : launch_rb_nt<CT, RB, GATHER, false>(p, g, nks, s);
-}
-
-// Row blocks of 16 per wave (VP3D_EXPAND_RB = 1..4 forces one): fewer rows per wave, fewer
-// VGPRs and less LDS per workgroup, more resident waves to hide store / input latency, but
-// the weight sweep is repeated for every workgroup.  Default: 4 where that instantiation
-// still holds 2 waves per SIMD (<= 256 VGPR + AGPR: the plain loader with K <= 128 — 250),
-// else 2 (the gathered loader's address arithmetic, or K up to 160, put RB = 4 at 280-327
-// registers = 1 wave per SIMD).  Measured at B = 8192: plain K = 102: 4 -> 0.370, 2 ->
-// 0.406, 1 -> 0.442 ms; gathered K = 138 (config 3): 4 -> 0.548, 3 -> 0.557, 2 -> 0.400 ms.
-int expand_rb(int nks, bool gather) {
-    static const int forced = [] {
-        const char* e = getenv("VP3D_EXPAND_RB");
-        const int r = e ? atoi(e) : 0;
-        return (r >= 1 && r <= 4) ? r : 0;
-    }();
-    if (forced) return forced;
-    return (!gather && nks <= 4) ? 4 : 2;
-}
-
+// Output stores are nontemporal when the output exceeds the 256 MB Infinity Cache: the
+// 1.36 GB output (B = 8192) cannot stay there anyway; streamed past it, it leaves the
+// caches to the weights and the block-1 conv that follows runs 1-1.5 % faster (3.10-3.12
+// vs 3.14-3.18 ms per step, A/B on one box).  A smaller output is left cached for the
+// next layer.
+//
+// Row blocks of 16 per wave: fewer rows per wave, fewer VGPRs and less LDS per
+// workgroup, more resident waves to hide store / input latency, but the weight sweep is
+// repeated for every workgroup.  4 where that instantiation still holds 2 waves per SIMD
+// (<= 256 VGPR + AGPR: the plain loader with K <= 128 — 250), else 2 (the gathered
+// loader's address arithmetic, or K up to 160, put RB = 4 at 280-327 registers = 1 wave
+// per SIMD).  Measured at B = 8192 (round 1): plain K = 102: RB 4 -> 0.370, 2 -> 0.406,
+// 1 -> 0.442 ms; gathered K = 138 (config 3): 4 -> 0.548, 3 -> 0.557, 2 -> 0.400 ms.
 template <typename CT, bool GATHER>
 hipError_t launch_t(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
-    switch (expand_rb(nks, GATHER)) {
-        case 1: return launch_rb<CT, 1, GATHER>(p, g, nks, s);
-        case 2: return launch_rb<CT, 2, GATHER>(p, g, nks, s);
-        case 3: return launch_rb<CT, 3, GATHER>(p, g, nks, s);
-        default: return launch_rb<CT, 4, GATHER>(p, g, nks, s);
-    }
+    const bool nt = (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
+    if (!GATHER && nks <= 4)
+        return nt ? launch_rb_nt<CT, 4, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 4, GATHER, false>(p, g, nks, s);
+    return nt ? launch_rb_nt<CT, 2, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 2, GATHER, false>(p, g, nks, s);
 }
 
 }  // namespace

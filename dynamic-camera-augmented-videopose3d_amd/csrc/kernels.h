@@ -47,27 +47,9 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
 bool conv_gemm_big_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_big(const ConvGemmParams& p, Act out_type, Act compute,
                                 hipStream_t stream);
-// Other schedules of the 256x256 tile (same eligibility, tile 256 only):
-// persistent grid (conv_gemm_persist.hip) and wave-group ping-pong (conv_gemm_pp.hip).
-// big_schedule(): VP3D_GEMM=big|persist|pp -> 0|1|2.
-int big_schedule();
-hipError_t launch_conv_gemm_persist(const ConvGemmParams& p, Act out_type, Act compute,
-                                    hipStream_t stream);
-hipError_t launch_conv_gemm_pp(const ConvGemmParams& p, Act out_type, Act compute, hipStream_t stream);
-
-// Persistent transposed-MFMA 256x256 kernel with register-direct epilogue
-// (conv_gemm_tp.hip): default for the large layers with 16-bit output
-// (VP3D_GEMM=big|persist|pp selects the older schedules for A/B runs).
-bool conv_gemm_tp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
-hipError_t launch_conv_gemm_tp(const ConvGemmParams& p, Act compute, hipStream_t stream);
-
 // Wave-group ping-pong 256x256 kernel with register-direct epilogue (conv_gemm_8p.hip).
 bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream);
-// Persistent form of the same kernel (conv_gemm_8pp.hip): one workgroup per CU, one
-// continuous LDS-DMA stream across its tiles (K >= 128).
-bool conv_gemm_8pp_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
-hipError_t launch_conv_gemm_8pp(const ConvGemmParams& p, Act compute, hipStream_t stream, bool dyn = false);
 // measurement only (VP3D_ABL=7 launches): 10 u64 timestamps/ids per workgroup
 hipError_t conv_gemm_8p_set_trace(unsigned long long* buf);
 

@@ -408,15 +408,6 @@ int vp3d_reserve(vp3d_handle* h, int B, int T, int dtype) {
     return ensure_ws(h, B, T, dtype);
 }
 
-// VP3D_EXPAND=pack selects the older pack-rows + generic GEMM expand path (A/B runs)
-static bool expand_gemm_env() {
-    static const bool on = [] {
-        const char* e = getenv("VP3D_EXPAND");
-        return !(e && !strcmp(e, "pack"));
-    }();
-    return on;
-}
-
 // The forward of B windows of T frames.  x: (B, T, J_in*F) f32, or nullptr with `gs`
 // describing where the windows are gathered from (vp3d_forward_windows).
 static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream,
@@ -502,7 +493,7 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         const Act o_type = last ? Act::F32 : act;
         hipError_t e = hipSuccess;
         bool launched = false;
-        if (first && gs && act != Act::F32 && expand_gemm_env() && expand_gather_eligible(p, *gs, o_type, act)) {
+        if (first && gs && act != Act::F32 && expand_gather_eligible(p, *gs, o_type, act)) {
             // the window gather (+ camera concat) fused into the expand conv's operand loads
             e = launch_expand_gemm_gather(p, *gs, act, s);
             launched = true;
@@ -523,13 +514,15 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
             p.A = x;
         }
         if (launched) {
-        } else if (first && act != Act::F32 && expand_gemm_env() && expand_gemm_eligible(p, o_type, act)) {
+        } else if (first && act != Act::F32 && expand_gemm_eligible(p, o_type, act)) {
             // 16-bit expand conv straight from the f32 input rows (expand_gemm.hip)
             e = launch_expand_gemm(p, act, s);
             launched = true;
         } else if (first && act != Act::F32) {
-            // 16-bit path: pack the f32 input rows of the expand conv into zero-padded
-            // 16-bit GEMM rows (one launch) so the conv runs on the tap-aligned kernel
+            // 16-bit path for the shapes expand_gemm does not take (K > 160: filter width 5
+            // and wider, or more input joints): pack the f32 input rows of the expand conv
+            // into zero-padded 16-bit GEMM rows (one launch) so the conv runs on the
+            // tap-aligned kernel
             void* packed = base + 3 * buf_elems * es;
             hipError_t pe = launch_pack_rows((const float*)x, p.M, p.T_out, p.T_in, p.stride, p.lda,
                                              p.K, p.Kp, packed, act == Act::BF16, s);

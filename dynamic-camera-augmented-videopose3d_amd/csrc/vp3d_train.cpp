@@ -62,6 +62,7 @@ struct vp3d_trainer {
     double* red = nullptr;
     float* coef = nullptr;
     float* wpart = nullptr;
+    int64_t wpart_floats = 0;  // >= every layer's N * K (one split of weight-gradient partials)
     // latest forward
     bool have_fwd = false;
     int B = 0, T = 0;
@@ -124,8 +125,15 @@ int reserve(vp3d_trainer* t, int B, int T) {
     floats += (size_t)max_dz;
     const size_t coef_off = floats;
     floats += 3 * (size_t)C;
+    // split-row weight-gradient partials: up to kWgradPartFloats, and never less than one
+    // whole N x K partial (the --dense k-conv of a 243-frame, 1024-channel model is
+    // 1024 x 163*1024 = 171 M floats; wgrad_splits never goes below one split)
+    int64_t max_nk = 0;
+    for (int l = 0; l < nl; ++l)
+        max_nk = std::max<int64_t>(max_nk, (int64_t)t->layers[l].cout * t->layers[l].taps * t->layers[l].cin);
+    const int64_t wpart_floats = std::max<int64_t>(kWgradPartFloats, max_nk);
     const size_t wpart_off = floats;
-    floats += (size_t)kWgradPartFloats;
+    floats += (size_t)wpart_floats;
     floats = (floats + 1) & ~(size_t)1;  // 8-byte alignment for the doubles
     const size_t red_off = floats;
     floats += 2 * (size_t)max_red;
@@ -148,6 +156,7 @@ int reserve(vp3d_trainer* t, int B, int T) {
     t->dZ = f + dz_off;
     t->coef = f + coef_off;
     t->wpart = f + wpart_off;
+    t->wpart_floats = wpart_floats;
     t->red = (double*)(f + red_off);
     return VP3D_OK;
 }
@@ -363,7 +372,9 @@ int vp3d_train_backward(vp3d_trainer* t, float* const* params, int n_params, con
         w.N = L.cout;
         w.K = L.taps * L.cin;
         w.part = t->wpart;
-        const int S = wgrad_splits(w.M, w.N, w.K, kWgradPartFloats);
+        if ((int64_t)w.N * w.K > t->wpart_floats)
+            return fail(VP3D_ERR_STATE, "weight-gradient partial buffer smaller than one N x K split");
+        const int S = wgrad_splits(w.M, w.N, w.K, t->wpart_floats);
         HIP_TRY(launch_wgrad(w, S, L.taps, dW, s));
         return VP3D_OK;
     };

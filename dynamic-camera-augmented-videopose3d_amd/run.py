@@ -28,6 +28,8 @@ import time  # noqa: E402
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from vp3d_amd.checkpoint import load_checkpoint  # noqa: E402
+
 
 def synthetic_dataset(args, normalize=None):
     """Seeded synthetic split (vp3d_amd.synth.synthetic_split); keypoints normalised
@@ -96,7 +98,7 @@ def build_model(args, J, announce=True):
     else:
         path = os.path.join(args.checkpoint, args.evaluate)
         print('Loading checkpoint', path)
-        ckpt = torch.load(path, map_location="cpu", weights_only=not args.trust_checkpoint)
+        ckpt = load_checkpoint(path, trust=args.trust_checkpoint)
         model.load_state_dict(ckpt["model_pos"])
     return model
 
@@ -204,8 +206,9 @@ def train_main(args, data):
     if args.resume:
         path = os.path.join(args.checkpoint, args.resume)
         print('Loading checkpoint', path)
-        # a run.py checkpoint holds the generator's numpy RandomState (run.py:566)
-        resume = torch.load(path, map_location="cpu", weights_only=False)
+        # a run.py checkpoint holds the generator's numpy RandomState (run.py:566): the
+        # weights-only loader admits exactly that (vp3d_amd.checkpoint)
+        resume = load_checkpoint(path, trust=args.trust_checkpoint)
         model_pos_train.load_state_dict(resume["model_pos"])
     optimizer = Adam(model_pos_train.parameters(), lr=args.learning_rate, amsgrad=True)
     train_generator = ChunkedGenerator(args.batch_size // args.stride, cams_tr, p3d_tr, p2d_tr, args.stride,
@@ -217,8 +220,11 @@ def train_main(args, data):
                                   trajectory=args.trajectory).next_epoch()
 
     print('INFO: Training on {} frames'.format(sum(p.shape[0] for p in p2d_tr)))
+    # Reference quirk kept for drop-in output: run.py:673 calls train() without lr /
+    # lr_decay, so the optimiser starts at -lr but decays by train()'s default 0.95 (-lrd
+    # is parsed and unused) and the logged lr starts at train()'s default 0.001.
     return train(args, args.epochs, train_generator, test_generator, model_pos_train, model_pos, optimizer,
-                 args.learning_rate, args.lr_decay, save_state=True, resume=resume)
+                 0.001, 0.95, save_state=True, resume=resume)
 
 
 def main(argv=None):

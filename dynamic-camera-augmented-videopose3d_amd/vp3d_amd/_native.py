@@ -45,6 +45,7 @@ EXPORTS = [
     "vp3d_profile_read", "vp3d_profile_reset", "vp3d_profile_layers", "vp3d_normalize_screen",
     "vp3d_image_coordinates", "vp3d_camera_matrices", "vp3d_world_to_camera",
     "vp3d_gather_windows", "vp3d_mpjpe_accumulate", "vp3d_pose_metrics", "vp3d_project_to_2d", "vp3d_last_error", "vp3d_abi_version",
+    "vp3d_build_hash",
     "vp3d_stream_create", "vp3d_stream_reset", "vp3d_stream_io", "vp3d_stream_step",
     "vp3d_stream_frames_seen", "vp3d_stream_graph_capture", "vp3d_stream_graph_launch",
     "vp3d_stream_destroy",
@@ -153,6 +154,7 @@ _SIGNATURES = {
     "vp3d_seq_sliding_window": (_int, [_vp, _vp, _vp, _int, _int, _vp, _vp]),
     "vp3d_last_error": (ctypes.c_char_p, []),
     "vp3d_abi_version": (_int, []),
+    "vp3d_build_hash": (ctypes.c_char_p, []),
 }
 
 
@@ -177,8 +179,23 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        _check_provenance(lib)
         _lib = lib
         return lib
+
+
+def _check_provenance(lib) -> None:
+    """The library must have been built from the sources beside it (when they are
+    present, as in the repository and its snapshot on the GPU box)."""
+    from . import build as _build
+    if not os.path.isdir(_build.CSRC):
+        return
+    want = _build.source_hash()
+    got = lib.vp3d_build_hash().decode()
+    if got != want:
+        raise ImportError(
+            f"vp3d: {_LIB_PATH} was built from other sources (library {got[:16]}, tree {want[:16]}); "
+            "rebuild with `python __graft_entry__.py build`")
 
 
 class NativeError(RuntimeError):

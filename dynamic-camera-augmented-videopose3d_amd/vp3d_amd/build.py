@@ -19,7 +19,9 @@ INCLUDE = os.path.join(REPO, "include")
 BUILD_DIR = os.path.join(ROOT_PKG, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libvp3d.so")
 
-SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_persist.hip", "conv_gemm_pp.hip", "expand_gemm.hip", "conv_gemm_tp.hip", "conv_gemm_8p.hip", "conv_gemm_8pp.hip", "preprocess.hip", "metrics.hip", "stream_step.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp", "vp3d_seq.cpp"]
+SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_8p.hip", "expand_gemm.hip", "preprocess.hip",
+           "metrics.hip", "stream_step.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp",
+           "vp3d_seq.cpp"]
 HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "gemm_common.h"), os.path.join(CSRC, "host.h"),
            os.path.join(INCLUDE, "vp3d.h")]
 ARCH = os.environ.get("VP3D_OFFLOAD_ARCH", "gfx950")
@@ -31,6 +33,41 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-I", INCLUDE, "-I", CSRC,
                 "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-value",
                 "-Wno-unused-result"]
+
+
+def _hashed_files():
+    """Every file the library is built from: the translation units, every header under
+    csrc/ and include/, and this build recipe itself."""
+    files = [os.path.join(CSRC, s) for s in SOURCES]
+    for d in (CSRC, INCLUDE):
+        files += sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hpp")))
+    files.append(os.path.abspath(__file__))
+    return files
+
+
+def source_hash() -> str:
+    """SHA-256 over (relative path, contents) of the sources, the target arch and the
+    compiler flags: the provenance string embedded in libvp3d.so (vp3d_build_hash)."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(("arch=" + ARCH + ";flags=" + " ".join(COMMON_FLAGS[:4] + COMMON_FLAGS[8:])).encode())
+    for f in _hashed_files():
+        h.update(os.path.relpath(f, REPO).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def embedded_hash(path: str = LIB_PATH):
+    """The source hash a built library carries (read from the file, without loading it)."""
+    import re
+    try:
+        with open(path, "rb") as f:
+            m = re.search(rb"VP3D_SRC_SHA256=([0-9a-f]{64})", f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 def _newer(src_paths, dst):
@@ -53,6 +90,9 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
     from concurrent.futures import ThreadPoolExecutor
 
     os.makedirs(BUILD_DIR, exist_ok=True)
+    want = source_hash()
+    if embedded_hash() != want:
+        force = True  # built from other sources (or by another recipe): rebuild everything
     objs, todo = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
@@ -76,6 +116,15 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
                 if verbose and out.strip():
                     print(out)
     if force or _newer(objs, LIB_PATH):
+        # provenance: one generated translation unit carrying the source hash
+        info_src = os.path.join(BUILD_DIR, "build_info.cpp")
+        info_obj = info_src + ".o"
+        with open(info_src, "w") as f:
+            f.write('// generated by vp3d_amd/build.py\n'
+                    f'static const char kTag[] = "VP3D_SRC_SHA256={want}";\n'
+                    'extern "C" const char* vp3d_build_hash(void) { return kTag + 16; }\n')
+        _run([HIPCC] + COMMON_FLAGS + ["-c", info_src, "-o", info_obj])
+        objs.append(info_obj)
         cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB_PATH] + objs
         if verbose:
             print("$", " ".join(cmd), flush=True)

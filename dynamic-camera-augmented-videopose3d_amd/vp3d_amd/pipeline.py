@@ -257,43 +257,28 @@ class DeviceSequences:
         return out
 
 
-class SyntheticTrajectoryBatcher:
-    """Config-3 workload: camera-trajectory-conditioned 243-frame windows built on
-    device from synthetic CMU-style sequences every step (K @ E of every frame +
-    the edge-clamped window gather with the 12-channel camera concat)."""
+class SyntheticWindowPool:
+    """The synthetic window source of the bench (configs 2-4) and the 16-bit trajectory
+    tests: `n_seq` random-walk 2D keypoint tracks (1280x720 pixels, normalised as
+    run.py:117 does) resident in HBM, optionally with per-frame procedural cameras
+    (CMU intrinsics, yaw + linear dolly: vp3d_amd.synth.camera_extrinsics), and a seeded
+    global table of (sequence, start) pairs.  Identical on every rank, so a global batch
+    is sharded by slicing the pair table (vp3d_amd.shard.shard_range) and each rank
+    gathers its own windows on device (the ChunkedGenerator gather, generators.py:102-137)."""
 
-    def __init__(self, B: int, window: int, seed: int = 0, device=None, n_seq: int = 64,
-                 seq_len: int = 2048):
+    def __init__(self, seed: int, device=None, cameras: bool = False, n_seq: int = 64, seq_len: int = 2048):
         from . import synth
-        rng = np.random.RandomState(seed)
         kps, cams = [], []
         for i in range(n_seq):
-            trk = synth.keypoint_tracks(seed, f"traj{i}", seq_len)
+            trk = synth.keypoint_tracks(seed, f"pool{i}", seq_len)
             kps.append((trk / 1280 * 2 - np.array([1, 720 / 1280])).astype(np.float32))
             cams.append({"intrinsics": synth.CMU_INTRINSICS,
-                         "extrinsics": synth.camera_extrinsics(seed, f"traj{i}", seq_len)})
-        self.seqs = DeviceSequences(kps, None, cams, device)
-        self.B, self.window, self.pad = B, window, (window - 1) // 2
-        n_sets = 4
-        pairs = np.stack([rng.randint(0, n_seq, size=(n_sets, B)),
-                          rng.randint(0, seq_len, size=(n_sets, B))], axis=-1).astype(np.int32)
-        self.pairs = torch.from_numpy(pairs).to(self.seqs.device)
-        self.buf = torch.empty((B, window, self.seqs.f2 + 12), dtype=torch.float32,
-                               device=self.seqs.device)
-        self.k = 0
+                         "extrinsics": synth.camera_extrinsics(seed, f"pool{i}", seq_len)})
+        self.seqs = DeviceSequences(kps, None, cams if cameras else None, device)
+        self.n_seq, self.seq_len, self.seed = n_seq, seq_len, seed
 
-    def next_pairs(self) -> torch.Tensor:
-        """Per-frame K @ E of every sequence, then the next (B, 2) window table: the
-        inputs of NativeLifter.forward_windows (gather fused into the expand conv)."""
-        self.seqs.refresh_cameras()
-        p = self.pairs[self.k % self.pairs.shape[0]]
-        self.k += 1
-        return p
-
-    def gather(self, pairs: torch.Tensor) -> torch.Tensor:
-        """The (B, window, 23, 2) input tensor of a window table (materialised)."""
-        self.seqs.gather(pairs, self.window, self.pad, "2d", concat_cams=True, out=self.buf)
-        return self.buf.view(self.B, self.window, -1, 2)
-
-    def next_batch(self) -> torch.Tensor:
-        return self.gather(self.next_pairs())
+    def global_pairs(self, G: int) -> np.ndarray:
+        """(G, 2) int32 (sequence, start frame) table, a pure function of the pool seed."""
+        rng = np.random.RandomState(self.seed + 1)
+        return np.stack([rng.randint(0, self.n_seq, size=G), rng.randint(0, self.seq_len, size=G)],
+                        axis=-1).astype(np.int32)

@@ -20,6 +20,7 @@ import ctypes
 from typing import List, Sequence
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _native as N
 
@@ -62,6 +63,9 @@ class NativeTrainer:
                                                  float(p), float(momentum), int(seed) & (2 ** 64 - 1),
                                                  y.data_ptr(), N.stream_ptr(self.device)),
                     "vp3d_train_forward")
+        # the running statistics were written through raw pointers: bump their version
+        # counters so caches keyed on them (the eval lifter's folded weights) see the change
+        increment_version([t for t in params if not t.requires_grad])
         self.generation += 1
         return y
 
@@ -124,18 +128,22 @@ class TrainStep(torch.autograd.Function):
         ctx.generation = trainer.generation
         ctx.trainable = trainable
         # x and the parameters must be the ones the backward sees (the trainer keeps the
-        # activations; torch's version counters catch in-place updates in between)
-        ctx.save_for_backward(x, *state)
+        # activations); the native Adam bumps the version counters of what it writes, so an
+        # optimiser step between this forward and its backward fails torch's saved-tensor check
+        # (the running statistics, which every train-mode forward rewrites, are held by
+        # reference only: a second forward is reported by the generation check below)
+        ctx.save_for_backward(x, *[t for t, tr in zip(state, trainable) if tr])
+        ctx.state = state
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, *state = ctx.saved_tensors
         trainer = ctx.trainer
         if trainer.generation != ctx.generation:
             raise RuntimeError("vp3d: another train-mode forward of this model ran before this backward; "
                                "the native trainer keeps the activations of the latest forward only")
-        grads = trainer.backward(state, dy, ctx.trainable)
+        ctx.saved_tensors  # version check of x and the trained parameters
+        grads = trainer.backward(ctx.state, dy, ctx.trainable)
         return (None, None, None, None, None, None, None, *grads)
 
 
@@ -202,4 +210,7 @@ class Adam(torch.optim.Optimizer):
                             _ptrs([s["exp_avg_sq"] for s in sts]), vmax, numel, float(group["lr"]),
                             float(beta1), float(beta2), float(group["eps"]), float(group["weight_decay"]),
                             step, 1 if amsgrad else 0, N.stream_ptr(dev)), "vp3d_adam_step")
+                    # written through raw pointers: make the in-place update visible to
+                    # autograd's saved-tensor checks and to the eval lifter's weight cache
+                    increment_version(chunk)
         return loss

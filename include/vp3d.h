@@ -357,6 +357,10 @@ int vp3d_pose_metrics(const float* pred, const float* target, int64_t n_frames, 
 
 const char* vp3d_last_error(void);
 int vp3d_abi_version(void);
+/* SHA-256 (hex) of the sources this library was built from: every csrc/ translation unit
+ * and header plus include/vp3d.h and the compiler flags (vp3d_amd/build.py source_hash).
+ * The Python loader refuses a library whose hash differs from the tree beside it. */
+const char* vp3d_build_hash(void);
 
 #ifdef __cplusplus
 }

@@ -4,8 +4,8 @@ Tolerances (stated per the north star, SURVEY.md §7 "Hard parts"):
   fp32  : |MPJPE(native, GT) - MPJPE(oracle, GT)| <= 1e-7 m (= 1e-4 mm) and every
           coordinate within 1e-5 m of the oracle (the reference's own fp32
           deviation from exact arithmetic is ~2e-7 m on these weights).
-  bf16 / fp16 : measured separately, loose gates (bf16 operands carry 8 bits of
-          mantissa): MPJPE delta <= 2 mm, every coordinate within 5 cm.
+  bf16 / fp16 : measured separately; gates about 3x the largest error measured on
+          MI355X over these cases (bf16 operands carry 8 mantissa bits, fp16 11).
 """
 import numpy as np
 import pytest
@@ -19,8 +19,10 @@ pytestmark = pytest.mark.gpu
 
 FP32_COORD_TOL = 1e-5
 FP32_MPJPE_TOL = 1e-7
-H16_COORD_TOL = 5e-2
-H16_MPJPE_TOL = 2e-3
+H16_TOL = {  # (max |coordinate delta|, |dMPJPE|) in metres
+    "bf16": (1.0e-2, 1.5e-4),
+    "fp16": (2.0e-3, 3.0e-5),
+}
 
 
 def _run(strided, B, T, fw=(3, 3, 3, 3, 3), causal=False, channels=1024, jin=17, jout=17,
@@ -47,8 +49,8 @@ def _check(y, ref, gt, dtype):
         assert err <= FP32_COORD_TOL, err
         assert d_mpjpe <= FP32_MPJPE_TOL, d_mpjpe
     else:
-        assert err <= H16_COORD_TOL, err
-        assert d_mpjpe <= H16_MPJPE_TOL, d_mpjpe
+        assert err <= H16_TOL[dtype][0], err
+        assert d_mpjpe <= H16_TOL[dtype][1], d_mpjpe
 
 
 @pytest.mark.parametrize("causal", [False, True])
@@ -66,15 +68,28 @@ def test_opt1f_243_h16(dtype):
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 def test_opt1f_243_h16_large_batch(dtype):
     # B = 2050 windows: the block-1/2 layers (M = 55,350 / 18,450 rows, the last
-    # 256-row tile partial) run on the persistent 256x256 kernel and the expand conv on
+    # 256-row tile partial) run on the 256x256 ping-pong kernel and the expand conv on
     # the fused expand kernel -- the kernels the headline bench times
     y, ref, gt = _run(True, 2050, 243, dtype=dtype)
     _check(y, ref, gt, dtype)
 
 
+@pytest.mark.parametrize("gemm", ["big", "8p"])
+def test_gemm_kernel_override(gemm, monkeypatch):
+    """Both 256x256 kernels on the shapes the default dispatch gives the other one:
+    VP3D_GEMM=big puts the strided block convs (B = 2050) on the LDS-ring kernel,
+    VP3D_GEMM=8p the dilated convs of a long sequence on the ping-pong kernel."""
+    monkeypatch.setenv("VP3D_GEMM", gemm)
+    if gemm == "big":
+        y, ref, gt = _run(True, 2050, 243, dtype="bf16")
+    else:
+        y, ref, gt = _run(False, 1, 20242, dtype="bf16")
+    _check(y, ref, gt, "bf16")
+
+
 def test_dilated_long_seq_bf16():
-    # one long sequence: every block layer has >= 256 output tiles, so the dilated
-    # taps (row offsets 0, d, 2d) and the residual slice run on the persistent kernel
+    # one long sequence: every block layer has >= 384 output tiles, so the dilated
+    # taps (row offsets 0, d, 2d) and the residual slice run on the LDS-ring kernel
     y, ref, gt = _run(False, 1, 20242, dtype="bf16")
     _check(y, ref, gt, "bf16")
 

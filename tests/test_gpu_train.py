@@ -199,6 +199,31 @@ def test_train_dropout_parity_with_oracle(strided, fw, B, T, channels):
             np.testing.assert_allclose(v.cpu().numpy(), st32[k], rtol=1e-5, atol=1e-6, err_msg=k)
 
 
+def test_train_dense_1024_large_wgrad():
+    """--dense at the full size (3,3,3,3,3, 1024 channels, 243 frames): the last k-conv has
+    163 taps, so one weight-gradient partial is 1024 x 166,912 floats (683 MB), larger than
+    the 256 MB split budget; the partial buffer is sized from the largest layer."""
+    meta = dict(strided=False, fw=[3, 3, 3, 3, 3], causal=False, dense=True, channels=1024)
+    from helpers import make_model
+    _, sd = make_model(False, (3, 3, 3, 3, 3), channels=1024, seed=9, dense=True)
+    m = _model(meta, sd)
+    B, T = 2, 243
+    x = synth.normalized_windows(6, "dense1024", B, T)
+    y = m(torch.from_numpy(x).cuda())
+    tgt = synth.normal(7, "dense1024/target", tuple(y.shape), std=0.2).astype(np.float32)
+    loss = torch.mean(torch.norm(y - torch.from_numpy(tgt).cuda(), dim=-1))
+    loss.backward()
+    torch.cuda.synchronize()
+    rm = _masks(m, B, T, "relu")
+    y32, l32, _, _ = _oracle(sd, x, tgt, meta)
+    _, _, g64, _ = _oracle(sd, x, tgt, meta, dtype=torch.float64, relu_masks=rm)
+    _, _, g32, _ = _oracle(sd, x, tgt, meta, relu_masks=rm)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), y32, atol=1e-5, rtol=0)
+    np.testing.assert_allclose(loss.item(), l32, rtol=1e-5)
+    for k, prm in m.named_parameters():
+        _grad_close(prm.grad.cpu().numpy(), g32[k], g64[k], k)
+
+
 def test_adam_kernel_bitexact_vs_torch():
     """vp3d_adam_step == torch.optim.Adam(amsgrad=True) (CPU, single-tensor path), 3 steps,
     tensors of assorted sizes (block tails, several tensors per launch)."""
@@ -235,6 +260,39 @@ def test_adam_kernel_bitexact_vs_torch():
     assert n_diff / n_all < 0.03, n_diff / n_all
     for i in sc:
         assert float(sg[i]["step"]) == float(sc[i]["step"]) == 3.0
+
+
+def test_native_writes_bump_versions():
+    """Adam and the running-stat update write through raw pointers; the version counters
+    move so (a) the eval lifter re-folds after a step, (b) a step between a forward and
+    its backward is caught by autograd's saved-tensor check."""
+    from vp3d_amd.train import Adam
+    g, meta, state = _load("train_dilated_c64")
+    m = _model(meta, state)
+    opt = Adam(m.parameters(), lr=meta["lr"], amsgrad=True)
+    x = torch.from_numpy(g["s0/x"]).cuda()
+    tgt = torch.from_numpy(g["s0/target"]).cuda()
+    loss = torch.mean(torch.norm(m(x) - tgt, dim=-1))
+    opt.zero_grad()
+    loss.backward()
+    m.eval()
+    with torch.no_grad():
+        y_before = m(x).clone()
+    opt.step()
+    with torch.no_grad():
+        y_after = m(x)
+    assert not torch.equal(y_before, y_after)  # the lifter saw the updated weights
+    # the eval output equals a fresh model built from the stepped state
+    fresh = _model(meta, {k: v.cpu().numpy() for k, v in m.state_dict().items()}).eval()
+    with torch.no_grad():
+        torch.testing.assert_close(fresh(x), y_after, rtol=0, atol=0)
+    m.train()
+    loss = torch.mean(torch.norm(m(x) - tgt, dim=-1))
+    opt.zero_grad()
+    loss.backward(retain_graph=True)
+    opt.step()
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        loss.backward()
 
 
 def test_train_errors():

@@ -1,9 +1,13 @@
 #!/bin/bash
-# Build the conv-GEMM check harness against the library's compiled objects.
+# Build the conv-GEMM check harness: the library's GEMM objects, with the 8p kernel
+# recompiled under -DVP3D_ABLATION so VP3D_ABL=1..4,7 select the ablated main loops
+# (measurement only; the product library never contains them).
 set -e
 cd "$(dirname "$0")"
 B=../../dynamic-camera-augmented-videopose3d_amd/build
-hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -I ../../include -I ../../dynamic-camera-augmented-videopose3d_amd/csrc \
-  -c gemm_check.hip -o /tmp/gemm_check.o
+CS=../../dynamic-camera-augmented-videopose3d_amd/csrc
+FL="-x hip --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I ../../include -I $CS"
+hipcc $FL -c gemm_check.hip -o /tmp/gemm_check.o
+hipcc $FL -DVP3D_ABLATION -c $CS/conv_gemm_8p.hip -o /tmp/conv_gemm_8p_abl.o
 hipcc --offload-arch=gfx950 -o gemm_check /tmp/gemm_check.o $B/conv_gemm.hip.o $B/conv_gemm_big.hip.o \
-  $B/conv_gemm_persist.hip.o $B/conv_gemm_pp.hip.o $B/conv_gemm_tp.hip.o $B/conv_gemm_8p.hip.o $B/conv_gemm_8pp.hip.o
+  /tmp/conv_gemm_8p_abl.o
