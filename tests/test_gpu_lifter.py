@@ -19,9 +19,9 @@ pytestmark = pytest.mark.gpu
 
 FP32_COORD_TOL = 1e-5
 FP32_MPJPE_TOL = 1e-7
-H16_TOL = {  # (max |coordinate delta|, |dMPJPE|) in metres
-    "bf16": (1.0e-2, 1.5e-4),
-    "fp16": (2.0e-3, 3.0e-5),
+H16_TOL = {  # (max |coordinate delta|, |dMPJPE|) in metres; measured maxima (MI355X, round 2):
+    "bf16": (1.0e-2, 1.5e-4),  # 3.56 mm (dilated 20,242-frame sequence), 0.057 mm
+    "fp16": (1.2e-3, 2.0e-5),  # 0.35 mm (B = 2050), 0.0058 mm
 }
 
 

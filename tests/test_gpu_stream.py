@@ -4,7 +4,7 @@ Reference semantics: UnchunkedGenerator pads a causal sequence with 2*pad copies
 of frame 0 in front (generators.py:193-198), and TemporalModel(causal=True) maps
 it to one pose per frame; pose k of the stream must equal frame k of that.
 Tolerances: fp32 stream (f32 FMA GEMVs) within 2e-5 m per coordinate; fp16
-weights within 0.3 mm (measured 0.087 mm, round 1), bf16 within 1 cm."""
+weights within 0.3 mm, bf16 within 3 mm (measured 0.14 / 0.90 mm, round 2)."""
 import numpy as np
 import pytest
 import torch
@@ -23,7 +23,7 @@ def _ref(sd, x, fw):
     return lifter_forward(sd, xp, list(fw), causal=True).numpy()[0]
 
 
-@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-5), ("fp16", 3e-4), ("bf16", 1e-2)])
+@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-5), ("fp16", 3e-4), ("bf16", 3e-3)])
 def test_stream_matches_sequence(dtype, tol):
     fw = (3, 3, 3, 3, 3)
     m, sd = make_model(False, fw, causal=True)
