@@ -8,11 +8,13 @@ evaluation).
     python run.py --evaluate synthetic --fcn-architecture 3,3,3 --subjects-test '*'
     python run.py --evaluate epoch_60.bin -c checkpoint --causal --compute-dtype bf16
 
-The reference reads hard-coded .npz paths (run.py:48,84) that ship nowhere, so the
-dataset here is a seeded synthetic CMU-style split (subjects x actions, procedural
-camera trajectories); .npz ingestion is §8(f) "next".  Sequences
-live in HBM (common.generators), the lifter is the native MI355X model
-(common.models.TemporalModel), Protocol #1 is the native mpjpe kernel.
+Data: `-d h36m | CMU | CMU_3DPW` reads the reference's .npz layout from --data-dir
+(data_3d_<d>.npz, data_2d_<d>_<keypoints>.npz; the reference hard-codes its paths,
+run.py:48,84) and prepares it as run.py:65-124 does (vp3d_amd.datasets); `-d synthetic`
+(default) is a seeded CMU-style split (subjects x actions, procedural camera
+trajectories).  Every action carries one entry per camera view
+(H36M: 4).  Sequences live in HBM (common.generators), the lifter is the native
+MI355X model (common.models.TemporalModel), Protocol #1 is the native mpjpe kernel.
 """
 from __future__ import annotations
 
@@ -32,13 +34,32 @@ from vp3d_amd.checkpoint import load_checkpoint  # noqa: E402
 
 
 def synthetic_dataset(args, normalize=None):
-    """Seeded synthetic split (vp3d_amd.synth.synthetic_split); keypoints normalised
-    on device by common.camera.normalize_screen_coordinates unless `normalize` is given."""
+    """Seeded synthetic split (vp3d_amd.synth.synthetic_split) in run.py's per-view form;
+    keypoints normalised on device by common.camera.normalize_screen_coordinates unless
+    `normalize` is given."""
     from vp3d_amd import synth
     if normalize is None:
         from common.camera import normalize_screen_coordinates as normalize
-    return synth.synthetic_split(args.synthetic_subjects, args.synthetic_actions,
-                                 args.synthetic_frames, args.joints, args.seed, normalize)
+    raw = synth.synthetic_split(args.synthetic_subjects, args.synthetic_actions,
+                                args.synthetic_frames, args.joints, args.seed, normalize)
+    return {s: {a: {k: [d[k]] for k in ("positions_3d", "keypoints", "cameras")} for a, d in acts.items()}
+            for s, acts in raw.items()}
+
+
+def load_data(args):
+    """The split run.py evaluates / trains on: synthetic or the reference's .npz files."""
+    from vp3d_amd.datasets import downsample, load_dataset
+    if args.dataset == "synthetic":
+        data = synthetic_dataset(args)
+    else:
+        _, data, _ = load_dataset(args.dataset, args.data_dir, args.keypoints)
+    return downsample(data, args.downsample)
+
+
+def joint_counts(data):
+    """(2D joints, 3D joints) of a prepared split."""
+    d = next(iter(next(iter(data.values())).values()))
+    return int(d["keypoints"][0].shape[-2]), int(d["positions_3d"][0].shape[-2])
 
 
 def group_actions(data, subjects):
@@ -60,9 +81,7 @@ def run_evaluation(data, actions, make_generator, model_fn, metrics, action_filt
         if action_filter is not None and not any(key.startswith(a) for a in action_filter):
             continue
         seqs = actions[key]
-        gen = make_generator([data[s][a]["cameras"] for s, a in seqs],
-                             [data[s][a]["positions_3d"] for s, a in seqs],
-                             [data[s][a]["keypoints"] for s, a in seqs])
+        gen = make_generator(*_views(data, seqs))
         res, e_seq, inf, mot = evaluate(gen, model_fn, metrics, key)
         per_action[key] = res
         for k, v in zip(("p1", "p2", "p3", "vel"), res):
@@ -81,12 +100,26 @@ def run_evaluation(data, actions, make_generator, model_fn, metrics, action_filt
     return {"per_action": per_action, "summary": summary, "pmcc": pmcc}
 
 
-def build_model(args, J, announce=True):
+def _views(data, seqs):
+    """(cameras, poses_3d, poses_2d) lists over every view of the (subject, action) pairs
+    (run.py:879-904 fetch_actions)."""
+    cams, p3d, p2d = [], [], []
+    for s, a in seqs:
+        d = data[s][a]
+        assert len(d["positions_3d"]) == len(d["keypoints"]) == len(d["cameras"]), "Camera count mismatch"
+        cams += d["cameras"]
+        p3d += d["positions_3d"]
+        p2d += d["keypoints"]
+    return cams, p3d, p2d
+
+
+def build_model(args, J, announce=True, J_out=None):
     from common.models.TemporalModel import TemporalModel
     from vp3d_amd import synth
     fw = [int(x) for x in args.fcn_architecture.split(",")]
+    J_out = J if J_out is None else J_out
     jin = J + 6 if args.trajectory else J
-    model = TemporalModel(jin, 2, J, filter_widths=fw, causal=args.causal, dropout=args.fcn_dropout,
+    model = TemporalModel(jin, 2, J_out, filter_widths=fw, causal=args.causal, dropout=args.fcn_dropout,
                           channels=args.channels, dense=args.dense)
     if announce:
         print('INFO: Receptive field: {} frames'.format(model.receptive_field()))
@@ -104,16 +137,11 @@ def build_model(args, J, announce=True):
 
 
 def fetch(data, subjects, action_filter=None):
-    """(cameras, poses_3d, poses_2d) lists of the given subjects (run.py:140-182)."""
-    cams, p3d, p2d = [], [], []
-    for s in subjects:
-        for a in data[s]:
-            if action_filter is not None and not any(a.startswith(f) for f in action_filter):
-                continue
-            cams.append(data[s][a]["cameras"])
-            p3d.append(data[s][a]["positions_3d"])
-            p2d.append(data[s][a]["keypoints"])
-    return cams, p3d, p2d
+    """(cameras, poses_3d, poses_2d) lists over every view of the given subjects
+    (run.py:126-182)."""
+    seqs = [(s, a) for s in subjects for a in data[s]
+            if action_filter is None or any(a.startswith(f) for f in action_filter)]
+    return _views(data, seqs)
 
 
 def train(args, n_epochs, train_generator, test_generator, model_pos_train, model_pos, optimizer,
@@ -196,8 +224,9 @@ def train_main(args, data):
     action_filter = None if args.actions == "*" else args.actions.split(",")
     print("Training Subjects: ", ", ".join(subjects_train))
     print("Test Subjects: ", ", ".join(subjects_test))
-    model_pos_train = build_model(args, args.joints).cuda()
-    model_pos = build_model(args, args.joints, announce=False).cuda()
+    j2, j3 = joint_counts(data)
+    model_pos_train = build_model(args, j2, J_out=j3).cuda()
+    model_pos = build_model(args, j2, announce=False, J_out=j3).cuda()
     pad = (model_pos.receptive_field() - 1) // 2
     causal_shift = pad if args.causal else 0
     cams_tr, p3d_tr, p2d_tr = fetch(data, subjects_train, action_filter)
@@ -237,11 +266,12 @@ def main(argv=None):
         raise SystemExit(f"--use-model {args.model_name}: only the FCN lifter runs on this path")
     if not torch.cuda.is_available():
         raise SystemExit("run.py evaluates on the MI355X (no CPU fallback)")
-    data = synthetic_dataset(args)
+    data = load_data(args)
     if not args.evaluate:
         return train_main(args, data)
     subjects = list(data.keys()) if args.subjects_test in (None, "*") else args.subjects_test.split(",")
-    model = build_model(args, args.joints).cuda().eval()
+    j2, j3 = joint_counts(data)
+    model = build_model(args, j2, J_out=j3).cuda().eval()
     model.set_compute_dtype(args.compute_dtype)
     pad = (model.receptive_field() - 1) // 2
     causal_shift = pad if args.causal else 0

@@ -343,7 +343,170 @@ def seq_lifter_goldens():
     seq_lifter_case("cam_lstm", "lstm")
 
 
-GROUPS = {"run_eval": run_eval_golden, "model": model_goldens, "generator": generator_goldens,
+DATASET_DIR = os.path.join(HERE, "datasets")
+H36M_SUBJECTS = ("S1", "S5")
+H36M_ACTIONS = ("Walking", "Walking 1", "Eating")
+CMU_SUBJECTS = ("01", "02")
+CMU_ACTIONS = ("walk_0", "jump_1")
+
+
+def write_dataset_fixtures():
+    """Small datasets in the reference's .npz layout (pickled dicts of arrays, as
+    prepare_data_h36m.py / prepare_data_cmu_camera.py write them): H36M world-space
+    32-joint mocap + per-camera 17-joint 2D tracks (some longer than the mocap, as in
+    the real data), and the fork's CMU camera-space poses + per-frame extrinsics."""
+    os.makedirs(DATASET_DIR, exist_ok=True)
+    # ---- Human3.6M ----
+    pos3, pos2 = {}, {}
+    for si, subj in enumerate(H36M_SUBJECTS):
+        pos3[subj], pos2[subj] = {}, {}
+        for ai, act in enumerate(H36M_ACTIONS):
+            T = 90 + 23 * ai + 11 * si
+            key = f"h36m/{subj}/{act}"
+            root = np.cumsum(synth.normal(11, key + "/root", (T, 1, 3), 0.01), axis=0) + np.array([0.0, 0.0, 0.9])
+            body = synth.normal(11, key + "/body", (1, 32, 3), 0.25)
+            jit = synth.normal(11, key + "/jit", (T, 32, 3), 0.005)
+            pos3[subj][act] = (root + body + jit).astype(np.float32)
+            pos2[subj][act] = [synth.keypoint_tracks(12, f"{key}/{c}", T + (3 if c == 1 else 0), 17, 1000, 1002)
+                               for c in range(4)]
+    meta = {"layout_name": "h36m", "num_joints": 17,
+            "keypoints_symmetry": [[4, 5, 6, 11, 12, 13], [1, 2, 3, 14, 15, 16]]}
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_3d_h36m.npz"), positions_3d=pos3)
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_2d_h36m_gt.npz"), positions_2d=pos2, metadata=meta)
+    # ---- CMU with procedural cameras ----
+    pos3, seqs, pos2 = {}, {}, {}
+    for si, subj in enumerate(CMU_SUBJECTS):
+        pos3[subj], seqs[subj], pos2[subj] = {}, {}, {}
+        for ai, act in enumerate(CMU_ACTIONS):
+            T = 100 + 31 * ai + 7 * si
+            key = f"cmu/{subj}/{act}"
+            p = synth.gt_poses(13, key, T, 17) + np.array([0.0, 0.0, 4.0], dtype=np.float32)
+            p = p + synth.normal(13, key + "/root", (T, 1, 3), 0.2).astype(np.float32)
+            pos3[subj][act] = p.astype(np.float32)
+            mot = synth.uniform(14, key, (4, 3), -1.0, 1.0)
+            seqs[subj][act] = {"cam_extrinsic": synth.camera_extrinsics(15, key, T), "cam_velocity": mot[0],
+                               "cam_acceleration": mot[1], "cam_angular_velocity": mot[2],
+                               "cam_angular_acceleration": mot[3],
+                               "pose_2d_flow": synth.normal(16, key, (T, 17, 2), 1.0).astype(np.float32)}
+            pos2[subj][act] = synth.keypoint_tracks(17, key, T, 17)
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_3d_CMU.npz"), positions_3d=pos3, cam_seqs=seqs)
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_2d_CMU_gt.npz"), positions_2d=pos2, metadata=meta)
+
+
+def _ref_eval(actions, fw, channels, seed, use_generator):
+    """The reference's evaluate() numbers per action key (run.py:697-771)."""
+    m, sd, keys = build_ref_model(False, fw, channels=channels, seed=seed)
+    pad = (m.receptive_field() - 1) // 2
+    out, e1_seq, infos, motion = {}, [], [], []
+    for key, (cams, p3d, p2d) in actions.items():
+        if use_generator:
+            batches = ref_gen.UnchunkedGenerator(cams, p3d, p2d, pad=pad, causal_shift=0).next_epoch()
+        else:
+            # the H36M camera records crash the reference generator (quirk Q1): the same
+            # batches, edge padding as generators.py:193-198
+            batches = ((None, p[None], np.pad(k, ((pad, pad), (0, 0), (0, 0)), "edge")[None],
+                        {"cam_velocity": np.zeros(3), "cam_acceleration": np.zeros(3),
+                         "cam_angular_velocity": np.zeros(3), "cam_angular_acceleration": np.zeros(3)})
+                       for p, k in zip(p3d, p2d))
+        e1 = e2 = e3 = ev = 0.0
+        N = 0
+        with torch.no_grad():
+            for bc, b3, b2, info in batches:
+                x2 = torch.from_numpy(b2.astype("float32"))
+                x3 = torch.from_numpy(b3.astype("float32"))
+                pred = m(x2)
+                err = ref_loss.mpjpe(pred, x3)
+                n = x3.shape[0] * x3.shape[1]
+                e3 += n * ref_loss.n_mpjpe(pred, x3).item()
+                e1 += n * err.item()
+                e1_seq.append(err.numpy())
+                infos.append(info)
+                motion.append(np.mean(np.linalg.norm(np.diff(b3, axis=1), axis=-1).squeeze(), axis=(0, 1)))
+                N += n
+                inp = x3.numpy().reshape(-1, x3.shape[-2], 3)
+                pr = pred.numpy().reshape(-1, x3.shape[-2], 3)
+                e2 += n * ref_loss.p_mpjpe(pr, inp)
+                ev += n * ref_loss.mean_velocity_error(pr, inp)
+        out[key] = np.array([(e1 / N) * 1000, (e2 / N) * 1000, (e3 / N) * 1000, (ev / N) * 1000])
+    return out
+
+
+def dataset_goldens():
+    """The reference's data preparation (run.py:47-124) on the fixture datasets, then its
+    evaluation loop: CMUMocapDataset + the reference generator as-is; H36M through the
+    importable pieces (Human36mDataset without the crashing joint removal, quirk Q1; the
+    reference Skeleton's remove_joints; world_to_camera; normalize_screen_coordinates)."""
+    import copy
+    from common.datasets import h36m_dataset as ref_h36m
+    from common.datasets.CMUMocapDataset import CMUMocapDataset
+    write_dataset_fixtures()
+    fw, channels, seed = [3, 3, 3], 256, 0
+    arrays = {}
+    # ---- CMU ----
+    ds = CMUMocapDataset(os.path.join(DATASET_DIR, "data_3d_CMU.npz"))
+    kp = np.load(os.path.join(DATASET_DIR, "data_2d_CMU_gt.npz"), allow_pickle=True)["positions_2d"].item()
+    for subj in ds.subjects():
+        for act in ds[subj].keys():
+            anim = ds[subj][act]
+            pos = anim["positions"]
+            pos -= pos[:, :1]
+            anim["positions_3d"] = [pos]
+    for subj in kp:
+        for act in kp[subj]:
+            k = kp[subj][act]
+            intr = ds.cameras()[subj][act]["intrinsics"]
+            k[..., :2] = ref_camera.normalize_screen_coordinates(k[..., :2], w=intr["res_w"], h=intr["res_h"])
+            kp[subj][act] = [k]
+    actions = {}
+    for subj in ds.subjects():
+        for act in ds[subj].keys():
+            c, p3, p2 = actions.setdefault(act.split(" ")[0], ([], [], []))
+            c.append(ds.cameras()[subj][act])
+            p3 += ds[subj][act]["positions_3d"]
+            p2 += kp[subj][act]
+            arrays[f"cmu/{subj}/{act}/p3d"] = ds[subj][act]["positions_3d"][0]
+            arrays[f"cmu/{subj}/{act}/kps"] = kp[subj][act][0]
+    res = _ref_eval(actions, fw, channels, seed, use_generator=True)
+    arrays["cmu_actions"] = np.array(list(res.keys()))
+    arrays["cmu_errors"] = np.stack(list(res.values()))
+    # ---- Human3.6M ----
+    ds = ref_h36m.Human36mDataset(os.path.join(DATASET_DIR, "data_3d_h36m.npz"), remove_static_joints=False)
+    sk = copy.deepcopy(ref_h36m.h36m_skeleton)
+    kept = sk.remove_joints([4, 5, 9, 10, 11, 16, 20, 21, 22, 23, 24, 28, 29, 30, 31])
+    kp = np.load(os.path.join(DATASET_DIR, "data_2d_h36m_gt.npz"), allow_pickle=True)["positions_2d"].item()
+    actions = {}
+    for subj in H36M_SUBJECTS:
+        for act in H36M_ACTIONS:
+            anim = ds[subj][act]
+            views3, views2 = [], []
+            for ci, cam in enumerate(anim["cameras"]):
+                p = ref_camera.world_to_camera(anim["positions"][:, kept], R=cam["orientation"], t=cam["translation"])
+                p[:, 1:] -= p[:, :1]
+                k = kp[subj][act][ci][:p.shape[0]].copy()
+                k[..., :2] = ref_camera.normalize_screen_coordinates(k[..., :2], w=cam["res_w"], h=cam["res_h"])
+                views3.append(p)
+                views2.append(k)
+                arrays[f"h36m/{subj}/{act}/{ci}/p3d"] = p
+                arrays[f"h36m/{subj}/{act}/{ci}/kps"] = k
+            c, p3, p2 = actions.setdefault(act.split(" ")[0], ([], [], []))
+            c += [None] * len(views3)
+            p3 += views3
+            p2 += views2
+    res = _ref_eval(actions, fw, channels, seed, use_generator=False)
+    arrays["h36m_actions"] = np.array(list(res.keys()))
+    arrays["h36m_errors"] = np.stack(list(res.values()))
+    for subj in H36M_SUBJECTS:
+        for ci, cam in enumerate(ds.cameras()[subj]):
+            for k in ("center", "focal_length", "translation", "orientation", "intrinsic"):
+                arrays[f"h36m_cam/{subj}/{ci}/{k}"] = np.asarray(cam[k])
+    arrays["h36m_skeleton_parents"] = np.asarray(sk.parents())
+    arrays["h36m_kept_joints"] = np.asarray(kept)
+    arrays["meta"] = np.array(json.dumps(dict(fw=fw, channels=channels, seed=seed,
+                                              h36m_subjects=list(H36M_SUBJECTS), cmu_subjects=list(CMU_SUBJECTS))))
+    save("run_eval_datasets", **arrays)
+
+
+GROUPS = {"run_eval": run_eval_golden, "dataset": dataset_goldens, "model": model_goldens, "generator": generator_goldens,
           "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens,
           "train": train_goldens, "seq_lifter": seq_lifter_goldens}
 

@@ -1,0 +1,124 @@
+"""Dataset ingestion: the reference's .npz layout, the H36M
+camera path (quirk Q1) and run.py's per-dataset preparation (run.py:47-124).
+
+Fixtures: tests/golden/datasets/*.npz are small datasets in the reference's layout
+(pickled dicts of arrays, written by make_golden.py); run_eval_datasets.npz holds
+what the reference's own code made of them (CMUMocapDataset + generator + model +
+losses as-is; Human36mDataset without its crashing joint removal, the reference
+Skeleton's remove_joints, world_to_camera and normalize_screen_coordinates).
+
+CPU: the restricted loader (no code runs), the dataset classes, skeleton and camera
+normalisation.  GPU: the full preparation (device normalisation and world_to_camera:
+bit-exact) and `run.main(['-d', 'h36m' | 'CMU', ...])` against the reference's
+per-action errors (Protocol #1 within 1e-4 mm).
+"""
+import json
+import os
+import pickle
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DATA = os.path.join(GOLD, "datasets")
+
+
+def _golden():
+    g = np.load(os.path.join(GOLD, "run_eval_datasets.npz"), allow_pickle=False)
+    return g, json.loads(str(g["meta"]))
+
+
+def test_loader_reads_reference_layout_without_code():
+    from vp3d_amd.npz_io import load_tree
+    pos = load_tree(os.path.join(DATA, "data_3d_h36m.npz"), "positions_3d")
+    assert set(pos) == {"S1", "S5"} and pos["S1"]["Walking"].shape[1:] == (32, 3)
+    kp = load_tree(os.path.join(DATA, "data_2d_h36m_gt.npz"), "positions_2d")
+    assert len(kp["S5"]["Eating"]) == 4 and kp["S5"]["Eating"][1].shape[1:] == (17, 2)
+    meta = load_tree(os.path.join(DATA, "data_2d_h36m_gt.npz"), "metadata")
+    assert meta["num_joints"] == 17
+
+
+def test_loader_refuses_code(tmp_path):
+    from vp3d_amd.npz_io import load_tree
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("echo pwned > " + str(tmp_path / "pwned"),))
+    path = str(tmp_path / "data_3d_evil.npz")
+    np.savez(path, positions_3d=np.array({"S1": {"a": Evil()}}, dtype=object))
+    with pytest.raises(pickle.UnpicklingError):
+        load_tree(path, "positions_3d")
+    assert not os.path.exists(tmp_path / "pwned")
+
+
+def test_h36m_dataset_skeleton_and_cameras():
+    """Joint removal 32 -> 17 (the reference's Skeleton, then the shoulder re-wiring of
+    h36m_dataset.py:250-251) and the normalised calibration (h36m_dataset.py:215-232)."""
+    from common.datasets.h36m_dataset import Human36mDataset
+    g, meta = _golden()
+    ds = Human36mDataset(os.path.join(DATA, "data_3d_h36m.npz"))
+    want = np.array(g["h36m_skeleton_parents"])
+    want[11] = want[14] = 8
+    np.testing.assert_array_equal(ds.skeleton_3d().parents(), want)
+    assert ds.skeleton_2d() is ds.skeleton_3d() and ds.skeleton_3d().num_joints() == 17
+    assert ds["S1"]["Walking"]["positions"].shape[1] == 17
+    raw = np.load(os.path.join(DATA, "data_3d_h36m.npz"), allow_pickle=True)["positions_3d"].item()
+    np.testing.assert_array_equal(ds["S5"]["Eating"]["positions"], raw["S5"]["Eating"][:, g["h36m_kept_joints"]])
+    for subj in meta["h36m_subjects"]:
+        for ci, cam in enumerate(ds.cameras()[subj]):
+            for k in ("center", "focal_length", "translation", "orientation", "intrinsic"):
+                np.testing.assert_array_equal(cam[k], g[f"h36m_cam/{subj}/{ci}/{k}"], err_msg=f"{subj} {ci} {k}")
+    # a second instance is unaffected by the first's joint removal (the reference edits a global)
+    assert Human36mDataset(os.path.join(DATA, "data_3d_h36m.npz")).skeleton_3d().num_joints() == 17
+
+
+def test_cmu_dataset_cameras():
+    from common.datasets.CMUMocapDataset import CMUMocapDataset
+    ds = CMUMocapDataset(os.path.join(DATA, "data_3d_CMU.npz"))
+    cam = ds.cameras()["01"]["walk_0"]
+    np.testing.assert_array_equal(cam["intrinsics"]["center"], np.zeros(2, np.float32))
+    assert cam["intrinsics"]["focal_length"].dtype == np.float32
+    np.testing.assert_allclose(cam["intrinsics"]["focal_length"], [1.5625, 1.5625])
+    assert cam["extrinsics"].shape == (ds["01"]["walk_0"]["positions"].shape[0], 3, 4)
+    assert ds.skeleton_2d().num_joints() == 17
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["h36m", "CMU"])
+def test_prepare_matches_reference(name):
+    """run.py:65-124 on the device: camera-space 3D (Q3 root handling per dataset, H36M
+    world_to_camera) and normalised 2D, bit-exact against the reference's preparation."""
+    from vp3d_amd.datasets import load_dataset
+    g, meta = _golden()
+    _, data, _ = load_dataset(name, DATA, "gt")
+    pre = "h36m" if name == "h36m" else "cmu"
+    n = 0
+    for subj, acts in data.items():
+        for act, d in acts.items():
+            for ci in range(len(d["keypoints"])):
+                key = f"h36m/{subj}/{act}/{ci}" if name == "h36m" else f"cmu/{subj}/{act}"
+                np.testing.assert_array_equal(d["positions_3d"][ci], g[key + "/p3d"], err_msg=key)
+                np.testing.assert_array_equal(d["keypoints"][ci], g[key + "/kps"], err_msg=key)
+                assert d["cameras"][ci]["extrinsics"].shape[0] == d["keypoints"][ci].shape[0]
+                n += 1
+    assert n == (len(meta["h36m_subjects"]) * 3 * 4 if name == "h36m" else 4), (pre, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["h36m", "CMU"])
+def test_run_main_dataset_matches_reference(name):
+    """`run.py -d <name> --evaluate` end to end on the MI355X (device generators, native
+    lifter fp32, native metrics) vs the reference's evaluation of the same files."""
+    import run
+    g, meta = _golden()
+    pre = "h36m" if name == "h36m" else "cmu"
+    want = dict(zip([str(a) for a in g[pre + "_actions"]], g[pre + "_errors"]))
+    res = run.main(["-d", name, "--data-dir", DATA, "-k", "gt", "--evaluate", "synthetic",
+                    "--fcn-architecture", ",".join(map(str, meta["fw"])), "--channels", str(meta["channels"]),
+                    "--seed", str(meta["seed"]), "--subjects-test", "*"])
+    assert set(res["per_action"]) == set(want)
+    for k, v in want.items():
+        got = np.asarray(res["per_action"][k])
+        print(name, k, got, v)
+        assert abs(got[0] - v[0]) <= 1e-4, (k, got[0], v[0])          # Protocol #1, mm
+        np.testing.assert_allclose(got[1:], v[1:], rtol=0, atol=1e-3)  # post-path protocols
