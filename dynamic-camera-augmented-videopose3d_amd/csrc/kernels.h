@@ -102,6 +102,35 @@ struct StreamLayerParams {
 };
 hipError_t launch_stream_gemv(const StreamLayerParams& q, Act wtype, hipStream_t s);
 
+// Causal streaming, persistent form (stream_persist.hip): one launch runs `steps` frames;
+// workgroup g owns channels [g*CPW, (g+1)*CPW) of every layer with their 16-bit weights
+// resident in LDS, the layer outputs handed to every workgroup through {tag, value}
+// granules.  Layers: 0 = expand, 2b-1 / 2b = block b's k-conv / 1x1, nl-1 = shrink.
+constexpr int kStreamMaxLayers = 16;
+constexpr int kStreamMaxTaps = 8;
+constexpr int kStreamMaxBlocks = 7;
+struct StreamPersistParams {
+    const void* W[kStreamMaxLayers];       // packed 16-bit weights [Np][Kp], tap-major K
+    const float* scale[kStreamMaxLayers];  // folded BatchNorm (shrink: 1 / bias)
+    const float* shift[kStreamMaxLayers];
+    int Kp[kStreamMaxLayers], N[kStreamMaxLayers];
+    int w_off[kStreamMaxLayers];           // LDS byte offset of each layer's CPW weight rows
+    int nl, nb, C, CPW, G, cin0;
+    int taps[kStreamMaxBlocks + 1], dil[kStreamMaxBlocks + 1], ring[kStreamMaxBlocks + 1];  // per block b >= 1
+    int x_off, xin_off, hist_off, part_off, ss_off;  // LDS byte offsets
+    int part_floats, state_floats;         // per workgroup
+    const float* frames;                   // frame queue (queue slots of cin0 floats)
+    int queue;
+    float* poses;                          // pose ring (queue slots of N[nl-1] floats)
+    int* frames_seen;                      // stream position (read at start, advanced at the end)
+    unsigned long long* gran;              // [2nb+1 edges][2 parities][C] granules, zeroed per launch
+    unsigned* err;                         // timeout word, zeroed per launch
+    float* state;                          // [G][state_floats]: partial-sum rings + frame history
+    int steps;
+};
+int stream_persist_lds_bytes();
+hipError_t launch_stream_persist(const StreamPersistParams& p, Act wtype, hipStream_t s);
+
 // preprocess kernels (preprocess.hip)
 hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, float* out,
                                    bool inverse, hipStream_t s);

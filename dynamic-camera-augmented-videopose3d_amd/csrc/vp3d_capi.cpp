@@ -649,6 +649,12 @@ struct vp3d_stream {
     std::vector<StreamLayerParams> steps;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
+    // persistent form (stream_persist.hip)
+    bool persist = false;
+    StreamPersistParams pp{};
+    void* hand = nullptr;              // [16 B: timeout word][granules], zeroed before each launch
+    size_t hand_bytes = 0;
+    float* pstate = nullptr;           // per-workgroup partial rings + frame history
 };
 
 namespace {
@@ -661,10 +667,100 @@ int pow2_at_least(int v) {
     return r;
 }
 
-int stream_launch(vp3d_stream* st, hipStream_t s) {
+// `steps` consecutive steps: one persistent launch (after zeroing its hand-off words), or
+// one GEMV launch per layer per step
+int stream_launch(vp3d_stream* st, hipStream_t s, int steps = 1) {
     const Act wt = st->dtype == VP3D_DTYPE_F32 ? Act::F32 : (st->dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16);
-    for (const StreamLayerParams& q : st->steps) HIP_TRY(launch_stream_gemv(q, wt, s));
+    if (st->persist) {
+        HIP_TRY(hipMemsetAsync(st->hand, 0, st->hand_bytes, s));
+        StreamPersistParams p = st->pp;
+        p.steps = steps;
+        HIP_TRY(launch_stream_persist(p, wt, s));
+        return VP3D_OK;
+    }
+    for (int i = 0; i < steps; ++i)
+        for (const StreamLayerParams& q : st->steps) HIP_TRY(launch_stream_gemv(q, wt, s));
     return VP3D_OK;
+}
+
+// The persistent form's geometry: one workgroup per CU, CPW channels each, every LDS
+// region 16-byte aligned.  False (the per-layer launches are used) when the model does
+// not fit: fp32 weights, an expand width other than 3, more than kStreamMaxTaps taps,
+// more than 4 channels per workgroup, or LDS over the kernel's budget.
+bool stream_persist_setup(vp3d_stream* st, int dtype) {
+    const vp3d_handle* h = st->h;
+    if (dtype == VP3D_DTYPE_F32) return false;
+    const char* mode = getenv("VP3D_STREAM_MODE");
+    if (mode && !strcmp(mode, "launches")) return false;
+    const int nl = (int)h->layers.size(), nb = h->cfg.n_widths - 1, C = h->cfg.channels;
+    if (nl > kStreamMaxLayers || nb < 1 || nb > kStreamMaxBlocks) return false;
+    if (h->layers[0].taps != 3 || h->layers[0].dil != 1) return false;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1)
+        return false;
+    int CPW = (C + cus - 1) / cus;
+    if (CPW > 4 || C % CPW) return false;
+    StreamPersistParams& p = st->pp;
+    p = StreamPersistParams{};
+    p.nl = nl;
+    p.nb = nb;
+    p.C = C;
+    p.CPW = CPW;
+    p.G = C / CPW;
+    p.cin0 = h->layers[0].cin;
+    const int nout = h->layers[nl - 1].cout;
+    if ((nout + CPW - 1) / CPW > p.G) return false;
+    auto a16 = [](int v) { return (v + 15) / 16 * 16; };
+    int off = 0;
+    for (int l = 0; l < nl; ++l) {
+        const Layer& L = h->layers[l];
+        if (L.Kp % 8) return false;
+        p.W[l] = dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh;
+        p.scale[l] = L.scale;
+        p.shift[l] = L.shift;
+        p.Kp[l] = L.Kp;
+        p.N[l] = L.cout;
+        p.w_off[l] = off;
+        off += a16(CPW * L.Kp * 2);
+    }
+    int part = 0;
+    for (int b = 1; b <= nb; ++b) {
+        const Layer& kc = h->layers[2 * b - 1];
+        if (kc.taps > kStreamMaxTaps || kc.Ktap != C || kc.K != kc.taps * C) return false;
+        p.taps[b] = kc.taps;
+        p.dil[b] = kc.dil;
+        p.ring[b] = pow2_at_least((kc.taps - 1) * kc.dil + 1);
+        part += p.ring[b] * CPW;
+    }
+    p.x_off = off;
+    off += a16(C * 4);
+    p.xin_off = off;
+    off += a16(h->layers[0].Kp * 4);
+    p.hist_off = off;
+    off += a16(2 * p.cin0 * 4);
+    p.part_off = off;
+    off += a16(part * 4);
+    p.ss_off = off;
+    off += a16(nl * 2 * CPW * 4);
+    if (off > stream_persist_lds_bytes()) return false;
+    p.part_floats = part;
+    p.state_floats = part + 2 * p.cin0;
+    p.frames = st->in_frame;
+    p.queue = kQueue;
+    p.poses = st->out_pose;
+    p.frames_seen = st->frames_seen;
+    st->hand_bytes = 16 + (size_t)(2 * nb + 1) * 2 * C * 8;
+    if (hipMalloc(&st->hand, st->hand_bytes) != hipSuccess) return false;
+    if (hipMalloc(&st->pstate, (size_t)p.G * p.state_floats * 4) != hipSuccess) {
+        hipFree(st->hand);
+        st->hand = nullptr;
+        return false;
+    }
+    hipMemset(st->pstate, 0, (size_t)p.G * p.state_floats * 4);
+    p.err = (unsigned*)st->hand;
+    p.gran = (unsigned long long*)((char*)st->hand + 16);
+    p.state = st->pstate;
+    return true;
 }
 
 }  // namespace
@@ -784,7 +880,19 @@ int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
         q.done_counter = (unsigned*)(st->frames_seen + 1);
         st->steps.push_back(q);
     }
+    st->persist = stream_persist_setup(st, dtype);
     *out = st;
+    return VP3D_OK;
+}
+
+int vp3d_stream_persistent(const vp3d_stream* st) { return st && st->persist ? 1 : 0; }
+
+int vp3d_stream_status(vp3d_stream* st) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (!st->persist) return VP3D_OK;
+    unsigned err = 0;
+    HIP_TRY(hipMemcpy(&err, st->hand, 4, hipMemcpyDeviceToHost));
+    if (err) return fail(VP3D_ERR_STATE, "persistent stream step timed out waiting for another CU");
     return VP3D_OK;
 }
 
@@ -840,9 +948,9 @@ int vp3d_stream_graph_capture(vp3d_stream* st, void* stream, int steps) {
         hipGraphDestroy(st->graph);
         st->graph = nullptr;
     }
+    if (st->persist && steps > kQueue) return fail(VP3D_ERR_ARG, "a persistent graph runs at most queue_len steps");
     HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    int rc = VP3D_OK;
-    for (int i = 0; i < steps && rc == VP3D_OK; ++i) rc = stream_launch(st, s);
+    int rc = stream_launch(st, s, steps);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(s, &g);
     if (rc) return rc;
@@ -869,6 +977,8 @@ int vp3d_stream_destroy(vp3d_stream* st) {
     hipFree(st->out_pose);
     hipFree(st->rings);
     hipFree(st->scratch);
+    hipFree(st->hand);
+    hipFree(st->pstate);
     delete st;
     return VP3D_OK;
 }

@@ -1,6 +1,9 @@
 """Causal streaming inference (BASELINE config 5): one 2D frame in, one 3D pose out.
 
-Wraps vp3d_stream (include/vp3d.h).  For a causal dilated TemporalModel
+Wraps vp3d_stream (include/vp3d.h): with 16-bit weights a batch of steps is one
+persistent launch (csrc/stream_persist.hip: weights resident in LDS, layer outputs
+handed between CUs in-launch), with fp32 weights one GEMV launch per layer
+(csrc/stream_step.hip).  For a causal dilated TemporalModel
 (reference TemporalModel.py:79-138 with causal=True), pose k of the stream equals
 frame k of the reference's whole-sequence evaluation of the edge-padded
 sequence (UnchunkedGenerator, generators.py:193-198, causal_shift = pad).
@@ -51,6 +54,17 @@ class CausalStream:
 
     def frames_seen(self) -> int:
         return int(self._lib.vp3d_stream_frames_seen(self._s))
+
+    @property
+    def persistent(self) -> bool:
+        """True when steps run as one persistent launch per batch (16-bit weights resident
+        in LDS); False for one GEMV launch per layer (fp32, or VP3D_STREAM_MODE=launches)."""
+        return bool(self._lib.vp3d_stream_persistent(self._s))
+
+    def check(self) -> None:
+        """Synchronise and raise if a persistent launch gave up waiting on another CU."""
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_stream_status(self._s), "vp3d_stream_status")
 
     # ---- hipGraph replay: steps read the device frame queue, write the pose ring ----
     def io_tensors(self):

@@ -169,6 +169,13 @@ int64_t vp3d_stream_frames_seen(vp3d_stream* s);
 int vp3d_stream_graph_capture(vp3d_stream* s, void* stream, int steps);
 int vp3d_stream_graph_launch(vp3d_stream* s, void* stream);
 int vp3d_stream_destroy(vp3d_stream* s);
+/* 1 when the stream runs as one persistent launch per batch of steps (16-bit weights
+ * resident in LDS, layer outputs handed between CUs in-launch), 0 for one GEMV launch
+ * per layer (fp32 weights, or VP3D_STREAM_MODE=launches at vp3d_stream_create). */
+int vp3d_stream_persistent(const vp3d_stream* s);
+/* Synchronises; VP3D_ERR_STATE if a persistent launch gave up waiting on another CU
+ * (bounded spins: the grid did not fit the device at once), else VP3D_OK. */
+int vp3d_stream_status(vp3d_stream* s);
 
 /* ---- training step (run.py:451-487, :662) ----
  * The reference trains TemporalModel in train mode: BatchNorm1d on batch

@@ -34,13 +34,40 @@ def test_stream_matches_sequence(dtype, tol):
     st = CausalStream(m.native_lifter(), dtype)
     xs = torch.from_numpy(x[0]).cuda()
     out = torch.stack([st.step(xs[t]).clone() for t in range(T)]).cpu().numpy()
+    st.check()
+    assert st.persistent == (dtype != "fp32")
     err = np.abs(out - ref).max()
-    print(f"stream {dtype}: max|d|={err:.3e} m")
+    print(f"stream {dtype} ({'persistent' if st.persistent else 'launches'}): max|d|={err:.3e} m")
     assert err <= tol
     assert st.frames_seen() == T
     st.reset()
     first = st.step(xs[0]).cpu().numpy()
     np.testing.assert_allclose(first, out[0], atol=1e-7)
+
+
+@pytest.mark.parametrize("fw,channels", [((3, 3, 3, 3, 3), 1024), ((3, 5, 3), 256)])
+def test_stream_launches_form_matches_sequence(fw, channels, monkeypatch):
+    """VP3D_STREAM_MODE=launches keeps the per-layer GEMV form for 16-bit weights; both
+    forms agree with the whole-sequence reference (width-5 block: general taps)."""
+    m, sd = make_model(False, fw, causal=True, channels=channels)
+    T = 120
+    x = synth.normalized_windows(13, "stream_forms", 1, T)
+    ref = _ref(sd, x, fw)
+    m.cuda()
+    xs = torch.from_numpy(x[0]).cuda()
+    outs = {}
+    for mode in ("launches", "persistent"):
+        if mode == "launches":
+            monkeypatch.setenv("VP3D_STREAM_MODE", "launches")
+        else:
+            monkeypatch.delenv("VP3D_STREAM_MODE", raising=False)
+        st = CausalStream(m.native_lifter(), "fp16")
+        assert st.persistent == (mode == "persistent")
+        outs[mode] = torch.stack([st.step(xs[t]).clone() for t in range(T)]).cpu().numpy()
+        st.check()
+        err = np.abs(outs[mode] - ref).max()
+        print(f"stream fp16 {mode} fw={fw}: max|d|={err:.3e} m")
+        assert err <= 3e-4
 
 
 def test_stream_graph_replay_matches_eager():
@@ -69,6 +96,7 @@ def test_stream_graph_replay_matches_eager():
                 for t in range(t0, t0 + G):
                     got.append(pr[t % Q].clone())
         torch.cuda.synchronize()
+        g.check()
         assert torch.equal(torch.stack(got), want), G
         assert g.frames_seen() == T
 
