@@ -330,6 +330,7 @@ int gemm_8p_mode() {
     const char* e = getenv("VP3D_GEMM");
     if (!e) return 1;
     if (strcmp(e, "8p") == 0) return 2;
+    if (strcmp(e, "q64") == 0) return 3;
     return strcmp(e, "big") == 0 ? 0 : 1;
 }
 bool gemm_8p_env(const ConvGemmParams& p) {
@@ -442,6 +443,9 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
             hipLaunchKernelGGL(conv_gemm_narrow<f16>, g, dim3(256), 0, stream, p);
         return hipGetLastError();
     }
+    if (gemm_8p_mode() == 3 && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
+        conv_gemm_q64_eligible(p, a_type, out_type, compute))
+        return launch_conv_gemm_q64(p, compute, stream);
     if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_8p_eligible(p, a_type, out_type, compute))
         return launch_conv_gemm_8p(p, compute, stream);

@@ -1,0 +1,262 @@
+// 256x256 conv-GEMM with 64-deep K-tiles staged as whole 128-byte lines, quadrant phases
+// and a wave-group ping-pong (16-bit operands, 16-bit output).
+//
+// Contract: ConvGemmParams (kernels.h), tap-aligned 16-bit activations (Ktap % 64 == 0):
+// the block k-convs and 1x1 convs of TemporalModel / TemporalModelOptimized1f (reference
+// common/models/TemporalModel.py:113-119, :129-135, :179-181, :191-195).
+//
+// Why: conv_gemm_8p stages 32-deep K-steps, so every LDS-DMA instruction fetches 16 rows
+// x 64 B — half cache lines — and its K loop measured ~54 % of the MFMA rate (0.94 us per
+// 32-deep step at block-1 shapes, tools/ubench/gemm_check trace), limited by the operand
+// stream (~42 GB/s per CU), not the MFMAs.  Here a DMA instruction moves 8 rows x 128 B,
+// whole lines (cdna_hip_programming.md §5, "x through LDS in full 128-B lines": fragment-
+// shaped 16 x 64-B pieces cost +18-45 %, TA_BUSY 2x).
+//
+// Geometry: 512 threads = 8 waves, wave (wr, wc) = (wid >> 2, wid & 3) owns rows
+// 128 wr .. +127 and channels 64 wc .. +63; MFMA v_mfma_f32_16x16x32 issued transposed
+// (D = W . A^T) so the epilogue is gemm::epilogue_tp (registers only).
+// LDS: 2 buffers x (A 256 rows + W 256 rows) x 128 B = 128 KiB; 16-byte chunk c of row r
+// stored at chunk c ^ ((r >> 1) & 7) (conflict-free ds_read_b128 for the fragment reads;
+// the swizzle is applied to each lane's SOURCE address, the DMA writes lane-linearly).
+//
+// K-tile t = 4 phases (quadrants of the wave's 128 x 64 tile: rows h, channels g):
+//   Q0 (h0, g0): read A_h0 (8 ds_read_b128) + W_g0 (4)   issue A_h0 of tile t+1
+//   Q1 (h0, g1): read W_g1 (4)                            issue W_g0 of t+1
+//   Q2 (h1, g1): read A_h1 (8)                            issue W_g1 of t+1
+//   Q3 (h1, g0): read W_g0 (4) again                      issue A_h1 of t+1
+// (W_g0 is re-read in Q3 rather than kept in 16 more VGPRs.)  A region (A_h* / W_g*) is re-staged >= 2 phases after its last
+// read, its reads retired before the barrier that ends their phase (WAR), and read 3
+// phases after its DMA was issued; each wave waits (vmcnt(4), never 0 in steady state) in the
+// memory segment of the phase BEFORE the one that reads the region, which precedes that
+// read by a barrier for both wave groups (RAW).  Each phase: [reads + 2 DMA pieces + wait]
+// barrier lgkmcnt(0) [16 MFMAs at s_setprio 1] barrier; wave group 1 runs one barrier
+// behind group 0, so the two waves of a SIMD alternate memory and MFMA segments.
+#include <cstdlib>
+
+#include "gemm_common.h"
+
+namespace vp3d {
+namespace {
+
+using namespace gemm;
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int QM = 256, QN = 256, QK = 64;
+constexpr int QBUF = (QM + QN) * QK * 2;  // 64 KiB per buffer
+constexpr int QW_OFF = QM * QK * 2;       // W region inside a buffer
+constexpr int QMAXN = 1024;
+
+__device__ __forceinline__ void qbarrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+__device__ __forceinline__ void qvm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <typename CT>
+__global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * QBUF + 2 * QMAXN * 4];
+    float* const s_scale = (float*)(smem + 2 * QBUF);
+    float* const s_shift = s_scale + QMAXN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wr = wid >> 2, wc = wid & 3;
+
+    for (int i = tid; i < p.N; i += 512) {
+        s_scale[i] = p.scale[i];
+        s_shift[i] = p.shift[i];
+    }
+
+    const int ntn = p.N / QN;
+    const int ntm = (p.M + QM - 1) / QM;
+    const int wg = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tile_m = wg / ntn;
+    const int tile_n = wg - tile_m * ntn;
+    const int m0 = tile_m * QM, n0 = tile_n * QN;
+
+    // ---- DMA pieces: 8 rows x 128 B each.  Region pieces (of 32 per operand):
+    //   A_h0 = {0..7, 16..23}, A_h1 = {8..15, 24..31}   (rows 64-row halves of each wave row)
+    //   W_g0 = {8c + 0..3},     W_g1 = {8c + 4..7}       (channel halves of each wave column)
+    // wave w issues two pieces of each region: A_h0 {w, 16+w}, A_h1 {8+w, 24+w},
+    // W_g0 {8(w>>2)+(w&3), 16+8(w>>2)+(w&3)}, W_g1 the same + 4.
+    // Lane l fills row 8q + (l >> 3), physical chunk (l & 7) = logical chunk lc ^ swz.
+    const int prow = lane >> 3;
+    auto lchunk = [&](int q) { return (lane & 7) ^ (((q & 1) * 4 + (prow >> 1)) & 7); };
+    int a_q[4];
+    a_q[0] = wid; a_q[1] = 16 + wid;          // A_h0
+    a_q[2] = 8 + wid; a_q[3] = 24 + wid;      // A_h1
+    int w_q[4];
+    w_q[0] = 8 * (wid >> 2) + (wid & 3); w_q[1] = w_q[0] + 16;  // W_g0
+    w_q[2] = w_q[0] + 4; w_q[3] = w_q[1] + 4;                  // W_g1
+    // every piece of a wave has the parity of wid (A) / of wid & 3 (W): one chunk each
+    const int a_lc = lchunk(wid), w_lc = lchunk(wid & 3);
+    int a_src[4], w_off[4];  // W extent Np * Kp < 2^31 elements
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        int m = m0 + 8 * a_q[j] + prow;
+        m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
+        a_src[j] = src_row(p, m);
+        w_off[j] = (n0 + 8 * w_q[j] + prow) * p.Kp + w_lc * 8;  // W rows padded to 256
+    }
+    const CT* A = (const CT*)p.A;
+    const CT* W = (const CT*)p.W;
+    // region r of tile s: 0 = A_h0, 1 = W_g0, 2 = W_g1, 3 = A_h1 (issue order)
+    auto issue = [&](int s, int r) {
+        char* buf = smem + (s & 1) * QBUF;
+        const int k0 = s * QK;
+        if (r == 0 || r == 3) {
+            const int j0 = r == 0 ? 0 : 2;
+            const int tap = k0 / p.Ktap;
+            const int cb = k0 - tap * p.Ktap;
+#pragma unroll
+            for (int j = j0; j < j0 + 2; ++j)
+                __builtin_amdgcn_global_load_lds(
+                    (gbl_ptr_t)(A + (int64_t)(a_src[j] + tap * p.dil) * p.lda + cb + a_lc * 8),
+                    (lds_ptr_t)(buf + a_q[j] * 1024), 16, 0, 0);
+        } else {
+            const int j0 = r == 1 ? 0 : 2;
+#pragma unroll
+            for (int j = j0; j < j0 + 2; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(W + w_off[j] + k0),
+                                                 (lds_ptr_t)(buf + QW_OFF + w_q[j] * 1024), 16, 0, 0);
+        }
+    };
+
+    // ---- fragment reads: row (l & 15) of a 16-row block, logical chunk 4 kh + (l >> 4),
+    // physical chunk ^ ((l & 15) >> 1) (row blocks start at multiples of 16) ----
+    const int fsw = (lane & 15) >> 1;
+    const int fo0 = (lane & 15) * 128 + (((lane >> 4) ^ fsw) << 4);        // kh = 0
+    const int fo1 = (lane & 15) * 128 + ((((lane >> 4) + 4) ^ fsw) << 4);  // kh = 1
+    const int a_base = wr * 128 * 128;
+    const int w_base = QW_OFF + wc * 64 * 128;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    u32x4 af[4][2];  // A fragments of the current row half: [row block][kh]
+    u32x4 bf[2][2];  // W fragments of the current channel half: [block jj][kh]
+
+    auto read_a = [&](const char* buf, int h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const char* r = buf + a_base + (h * 64 + i * 16) * 128;
+            af[i][0] = *(const u32x4*)(r + fo0);
+            af[i][1] = *(const u32x4*)(r + fo1);
+        }
+    };
+    auto read_w = [&](const char* buf, int g) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const char* r = buf + w_base + (g * 32 + jj * 16) * 128;
+            bf[jj][0] = *(const u32x4*)(r + fo0);
+            bf[jj][1] = *(const u32x4*)(r + fo1);
+        }
+    };
+    auto mma = [&](int h, int g) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+                    acc[4 * h + i][2 * g + jj] = mfma16<CT>(bf[jj][kh], af[i][kh], acc[4 * h + i][2 * g + jj]);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto compute_seg = [&](int h, int g) {
+        qbarrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mma(h, g);
+        qbarrier();
+    };
+
+    const int nk = p.Kp / QK;
+    // prologue: tile 0 whole (A_h0, W_g0, W_g1, A_h1); A_h0 and W_g0 landed
+    issue(0, 0);
+    issue(0, 1);
+    issue(0, 2);
+    issue(0, 3);
+    qvm<4>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scale / shift stores
+    qbarrier();
+    if (wr == 1) qbarrier();  // group 1 runs one barrier behind group 0
+
+    for (int t = 0; t < nk; ++t) {
+        const char* buf = smem + (t & 1) * QBUF;
+        const bool more = t + 1 < nk;
+        // ---- Q0: A_h0 + W_g0; stage A_h0(t+1); wait W_g1(t) ----
+        read_a(buf, 0);
+        read_w(buf, 0);
+        if (more) {
+            issue(t + 1, 0);
+            qvm<4>();  // W_g1(t) landed: younger A_h1(t), A_h0(t+1)
+        } else {
+            qvm<2>();  // younger: A_h1(t)
+        }
+        compute_seg(0, 0);
+        // ---- Q1: W_g1; stage W_g0(t+1); wait A_h1(t) ----
+        read_w(buf, 1);
+        if (more) {
+            issue(t + 1, 1);
+            qvm<4>();  // younger: A_h0(t+1), W_g0(t+1)
+        } else {
+            qvm<0>();
+        }
+        compute_seg(0, 1);
+        // ---- Q2: A_h1; stage W_g1(t+1) ----
+        read_a(buf, 1);
+        if (more) issue(t + 1, 2);
+        compute_seg(1, 1);
+        // ---- Q3: W_g0 again; stage A_h1(t+1); wait A_h0(t+1), W_g0(t+1) ----
+        read_w(buf, 0);
+        if (more) {
+            issue(t + 1, 3);
+            qvm<4>();  // younger: W_g1(t+1), A_h1(t+1)
+        }
+        compute_seg(1, 0);
+    }
+    if (wr == 0) qbarrier();  // match group 1's extra barrier
+
+    const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.ldy * sizeof(CT)));
+    // the residual (1x1 convs) is loaded inside the epilogue, one row block ahead of its use
+    if (p.R)
+        epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc);
+    else
+        epilogue_tp<CT, 8, false, 0, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc);
+}
+
+}  // namespace
+
+bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
+    if (compute == Act::F32 || a_type != compute || out_type != compute) return false;
+    if (p.Ktap % QK != 0 || p.Kp % QK != 0 || p.lda % 8 != 0) return false;
+    if (p.N % QN != 0 || p.N > QMAXN || p.ldy % 8 != 0 || (p.R && p.ldr % 8 != 0)) return false;
+    if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
+        (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
+        return false;
+    if ((size_t)p.M * p.ldy * 2 >= (1u << 31)) return false;  // 32-bit buffer offsets
+    if (p.R && (size_t)((p.M + p.T_out - 1) / p.T_out) * p.R_T * p.ldr * 2 >= (1u << 31)) return false;
+    return true;
+}
+
+hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream) {
+    const dim3 grid(((p.M + QM - 1) / QM) * (p.N / QN));
+    if (compute == Act::BF16)
+        hipLaunchKernelGGL((conv_gemm_q64<__bf16>), grid, dim3(512), 0, stream, p);
+    else
+        hipLaunchKernelGGL((conv_gemm_q64<_Float16>), grid, dim3(512), 0, stream, p);
+    return hipGetLastError();
+}
+
+}  // namespace vp3d

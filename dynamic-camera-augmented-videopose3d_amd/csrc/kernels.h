@@ -50,6 +50,9 @@ hipError_t launch_conv_gemm_big(const ConvGemmParams& p, Act out_type, Act compu
 // Wave-group ping-pong 256x256 kernel with register-direct epilogue (conv_gemm_8p.hip).
 bool conv_gemm_8p_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t stream);
+// 64-deep K-tiles staged as whole 128-byte lines, quadrant phases (conv_gemm_q64.hip).
+bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
+hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream);
 // measurement only (VP3D_ABL=7 launches): 10 u64 timestamps/ids per workgroup
 hipError_t conv_gemm_8p_set_trace(unsigned long long* buf);
 
