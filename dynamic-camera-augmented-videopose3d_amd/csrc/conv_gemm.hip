@@ -316,14 +316,16 @@ hipError_t launch_f32(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t
 }
 
 // Which 256x256 kernel a large layer runs on:
-//   default: the ping-pong kernel (conv_gemm_8p.hip) for contiguous-tap layers (the
-//   strided k-tap convs: 1.20 vs 1.22 ms on block 1 at B = 8192; the 1x1 convs with a
-//   residual: 0.54 vs 0.59 ms), the LDS-ring kernel (conv_gemm_big.hip) for dilated convs
-//   (taps gathered from rows d apart; sequence mode, 65,536 frames: 0.39-0.40 vs 0.42 ms).
-//   VP3D_GEMM=8p -> 8p wherever eligible, VP3D_GEMM=big -> the LDS-ring kernel everywhere
-//   (both kernels are on the default path, so both forms are parity-tested).  The round-1
-//   A/B schedules (persistent, dynamic-queue, older ping-pong, transposed persistent) were
-//   3-10 % slower and now live outside the library, in tools/ubench/retired/.
+//   default: for contiguous-tap layers (the strided k-tap convs and the 1x1 convs) the
+//   64-deep whole-line kernel (conv_gemm_q64.hip; block 1 at B = 8192 on one device, same
+//   process: k3 1.32-1.37 vs 1.37-1.39 ms for the ping-pong kernel, 1x1 + residual
+//   0.66-0.68 vs 0.67-0.70), then the ping-pong kernel (conv_gemm_8p.hip) where q64 is not
+//   eligible; the LDS-ring kernel (conv_gemm_big.hip) for dilated convs (taps gathered
+//   from rows d apart; sequence mode, 65,536 frames: 0.39-0.40 vs 0.42 ms).
+//   VP3D_GEMM=q64 / 8p -> that kernel wherever eligible (dilated layers included),
+//   VP3D_GEMM=big -> the LDS-ring kernel everywhere; the override test runs all three.
+//   The round-1 A/B schedules (persistent, dynamic-queue, older ping-pong, transposed
+//   persistent) were 3-10 % slower and live outside the library, in tools/ubench/retired/.
 //   Read at every launch (a getenv per layer is noise next to the kernel), so a test can
 //   flip it within one process.
 int gemm_8p_mode() {
@@ -443,7 +445,8 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
             hipLaunchKernelGGL(conv_gemm_narrow<f16>, g, dim3(256), 0, stream, p);
         return hipGetLastError();
     }
-    if (gemm_8p_mode() == 3 && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
+    const int gm = gemm_8p_mode();
+    if ((gm == 3 || (gm == 1 && p.dil == 1)) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_q64_eligible(p, a_type, out_type, compute))
         return launch_conv_gemm_q64(p, compute, stream);
     if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&

@@ -68,19 +68,19 @@ def test_opt1f_243_h16(dtype):
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 def test_opt1f_243_h16_large_batch(dtype):
     # B = 2050 windows: the block-1/2 layers (M = 55,350 / 18,450 rows, the last
-    # 256-row tile partial) run on the 256x256 ping-pong kernel and the expand conv on
-    # the fused expand kernel -- the kernels the headline bench times
+    # 256-row tile partial) run on the 256x256 whole-line kernel (q64) and the expand
+    # conv on the fused expand kernel -- the kernels the headline bench times
     y, ref, gt = _run(True, 2050, 243, dtype=dtype)
     _check(y, ref, gt, dtype)
 
 
-@pytest.mark.parametrize("gemm", ["big", "8p"])
-def test_gemm_kernel_override(gemm, monkeypatch):
-    """Both 256x256 kernels on the shapes the default dispatch gives the other one:
-    VP3D_GEMM=big puts the strided block convs (B = 2050) on the LDS-ring kernel,
-    VP3D_GEMM=8p the dilated convs of a long sequence on the ping-pong kernel."""
+@pytest.mark.parametrize("gemm,opt1f", [("big", True), ("8p", True), ("8p", False), ("q64", False)])
+def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
+    """Every 256x256 kernel on the shapes the default dispatch gives another one:
+    VP3D_GEMM=big / 8p put the strided block convs (B = 2050) on the LDS-ring / ping-pong
+    kernel, VP3D_GEMM=8p / q64 the dilated convs of a long sequence on those kernels."""
     monkeypatch.setenv("VP3D_GEMM", gemm)
-    if gemm == "big":
+    if opt1f:
         y, ref, gt = _run(True, 2050, 243, dtype="bf16")
     else:
         y, ref, gt = _run(False, 1, 20242, dtype="bf16")

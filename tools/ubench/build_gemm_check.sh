@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")"
 B=../../dynamic-camera-augmented-videopose3d_amd/build
 CS=../../dynamic-camera-augmented-videopose3d_amd/csrc
-FL="-x hip --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I ../../include -I $CS -Wno-unused-result"
+FL="-x hip --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I ../../include -I $CS -Wno-unused-result -Wno-unused-value"
 hipcc $FL -c gemm_check.hip -o /tmp/gemm_check.o
 hipcc $FL -DVP3D_ABLATION -c $CS/conv_gemm_8p.hip -o /tmp/conv_gemm_8p_abl.o
 hipcc --offload-arch=gfx950 -o gemm_check /tmp/gemm_check.o $B/conv_gemm.hip.o $B/conv_gemm_big.hip.o \

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")"
 G="timeout -k 5 60 ./gemm_check"
 M=221184
-for k in q64 8p; do
+for k in ${KERNS:-q64 8p}; do
   $G $k $M 1024 1024 1 1 0 | tail -2 || exit $?
   $G $k $M 1024 1024 1 1 1 | tail -2 || exit $?
   $G $k $M 1024 1024 1 3 0 | tail -2 || exit $?
