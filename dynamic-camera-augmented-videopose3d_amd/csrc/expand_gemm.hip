@@ -9,24 +9,25 @@
 //
 // Why a kernel of its own: K is tiny (102, or 138 with the camera concat) and
 // N = 1024, so the layer is bound by writing its (M x 1024) 16-bit output, not by
-// MFMA.  The generic path (pack f32 rows to padded 16-bit rows, then a 256x256
-// GEMM with 4 K-steps) spent ~0.75 ms at B = 8192 on what is ~1.6 GB of HBM
-// traffic.  Here:
+// MFMA.  Here:
 //   * A (the input rows) is read once, straight from the f32 input into MFMA
 //     fragments in VGPRs (8-byte loads, converted to bf16/f16 in registers): no
 //     packed copy in HBM, no A in LDS;
-//   * one workgroup (4 waves) owns 256 rows and sweeps all N = 1024 output
-//     channels in chunks of 64; the weights (<= 384 KB, L2-resident) stream
-//     through a double-buffered LDS chunk shared by the 4 waves;
-//   * the MFMA is issued transposed (D = W . A^T: v_mfma_f32_16x16x32 with the
-//     weight fragment as the A operand), so each lane's accumulator holds 4
-//     consecutive channels of one row: BN affine + ReLU + 16-bit convert in
-//     registers, one 8-byte write per (row block, channel block) into a
-//     wave-private LDS tile, then 16-byte stores of whole 128-byte lines
-//     (8 rows x 128 B per instruction).  The store path, not the MFMA, sets this
-//     kernel's speed: with 8-byte stores straight from the accumulators (16 rows
-//     x 32 B per instruction) the TA was busy 80 % of the kernel at ~120 cycles
-//     per store instruction (rocprofv3 TA_BUSY / TA_FLAT_WRITE_WAVEFRONTS).
+//   * one workgroup (4 waves) owns 64*RB rows and sweeps all N = 1024 output
+//     channels in chunks of 64; the weights (<= 320 KB, L2-resident) stream through a
+//     3-deep LDS ring of chunks, filled by LDS-DMA two chunks ahead (no VGPR staging);
+//   * the eval BatchNorm is folded into the 16-bit weights the host prepares for this
+//     kernel (Layer::wfbf / wfh: W * scale rounded once, shift as two 16-bit columns
+//     hi + lo at k = K, K + 1 that the loader feeds with 1.0), so the epilogue is a
+//     packed convert + a packed integer max for the ReLU (16-bit floats order like
+//     sign-magnitude integers: max(bits, 0) is relu, -0 included) -- 1 VALU op per
+//     output instead of 3.5 (scale, shift, max, convert: the old epilogue cost 0.6 ms
+//     of 3.1 at B = 65,536; with no stores at all the old kernel still took 2.9 ms);
+//   * the MFMA is issued transposed (D = W . A^T), so each lane's accumulator holds 4
+//     consecutive channels of one row; they go to a wave-private LDS tile and out as
+//     16-byte stores of whole 128-byte lines (8 rows x 128 B per instruction);
+//   * the chunk loop ends on a raw barrier with a counted vmcnt (the weight DMA of the
+//     next chunk only): the output stores stay in flight across chunks.
 #include <cstdlib>
 
 #include "gemm_common.h"
@@ -37,55 +38,72 @@ namespace {
 using namespace gemm;
 
 constexpr int kExpWaves = 4;
-constexpr int kExpChunkN = 64;                          // output channels per chunk
+constexpr int kExpChunkN = 64;  // output channels per chunk
 constexpr int kExpMaxN = 1024;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+constexpr int kExpRing = 3;     // weight chunks resident (current, next, next-but-one)
+constexpr int kExpSlab = 4096;  // bytes of one [64 channels][32 k] slab
+#ifdef VP3D_ABLATION
+__device__ int g_expand_abl;
+#endif
 
-// LDS layout of one weight chunk: NKS slabs of [64 channels][32 k] (64-byte rows),
-// 16-byte chunk c of row r stored at chunk (c + 2*((r>>2)&3)) & 3 -> the fragment
-// reads (row l&15 of a 16-row block, chunk l>>4) are bank-conflict free.
-__device__ __forceinline__ int exp_swz(int r, int c) { return r * 4 + ((c + 2 * ((r >> 2) & 3)) & 3); }
+// two f32 -> two 16-bit floats (round to nearest even) in one dword, element 0 low:
+// one v_cvt_pk_{bf16,f16}_f32 (compiler-generated, so the MFMA-result read hazard is
+// handled by the compiler)
+template <typename CT>
+__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
+    typedef float float2v __attribute__((ext_vector_type(2)));
+    typedef CT ct2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(float2v{a, b}, ct2));
+}
+
+template <int N>
+__device__ __forceinline__ void exp_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // RB = row blocks of 16 per wave (64 * RB rows per workgroup).
 // GATHER: the input rows are not a (B, T, Cin) tensor but windows of device-resident
 // sequences, gathered here (GatherSrc, kernels.h): the ChunkedGenerator batch and the
 // camera concat fused into the operand loader.
+// LDS image of a weight chunk: NKS slabs of [64 channels][32 k] (64-byte rows); the
+// 16-byte unit c' of row r holds k-chunk (c' - 2 ((r >> 2) & 3)) & 3, so the fragment
+// reads (row l & 15 of a 16-row block, k-chunk l >> 4) are bank-conflict free.  The DMA
+// writes a slab lane-linearly (wave w: rows 16w .. 16w + 15); the permutation is applied
+// to the global source address.
 template <typename CT, int NKS, int RB, bool GATHER, bool NT = false>
-__global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
-    constexpr int kExpRowsPerWave = 16 * RB;
-    constexpr int kExpRows = kExpRowsPerWave * kExpWaves;
-    constexpr int SLAB = kExpChunkN * 4;       // 16-byte units per k-step slab
-    constexpr int CHUNK_U = NKS * SLAB;        // 16-byte units per weight chunk
-    __shared__ __attribute__((aligned(16))) u32x4 wbuf[2][CHUNK_U];
-    __shared__ __attribute__((aligned(16))) float s_scale[kExpMaxN];
-    __shared__ __attribute__((aligned(16))) float s_shift[kExpMaxN];
-    // per-wave output staging: 64 rows x 128 B, 16-byte chunk c of row r at c ^ (r & 7)
-    __shared__ __attribute__((aligned(16))) u32x4 s_out[kExpWaves][kExpRowsPerWave * 8];
+__global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
+    constexpr int kRowsW = 16 * RB;
+    constexpr int kRows = kRowsW * kExpWaves;
+    constexpr int kChunk = NKS * kExpSlab;
+    // ring of weight chunks, then per-wave output staging: kRowsW rows x 128 B, 16-byte
+    // unit c of row r at c ^ (r & 7)
+    __shared__ __attribute__((aligned(16))) char smem[kExpRing * kChunk + kExpWaves * kRowsW * 128];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
-    const int m_wave = blockIdx.x * kExpRows + wid * kExpRowsPerWave;
+    const int m_wave = blockIdx.x * kRows + wid * kRowsW;
+    u32x4* const stage = (u32x4*)(smem + kExpRing * kChunk + wid * kRowsW * 128);
 
-    for (int i = tid; i < p.N; i += 256) {
-        s_scale[i] = p.scale[i];
-        s_shift[i] = p.shift[i];
-    }
-
-    // ---- weight chunk staging: NKS 16-byte pieces per thread ----
-    const CT* W = (const CT*)p.W;
-    const int st_row = tid >> 2, st_c = tid & 3;
-    u32x4 wst[NKS];
-    auto wload = [&](int chunk) {
-        const CT* src = W + (int64_t)(chunk * kExpChunkN + st_row) * p.Kp + st_c * 8;
+    // ---- weight chunk DMA: NKS pieces of 1 KB per wave ----
+    const int dr = 16 * wid + (lane >> 2);
+    const int dc = ((lane & 3) - 2 * ((dr >> 2) & 3)) & 3;
+    const CT* const wsrc = (const CT*)p.W + (int64_t)dr * p.Kp + dc * 8;
+    auto stage_w = [&](int chunk) {
+        char* dst = smem + (chunk % kExpRing) * kChunk + wid * 1024;
+        const CT* src = wsrc + (int64_t)chunk * kExpChunkN * p.Kp;
 #pragma unroll
-        for (int q = 0; q < NKS; ++q) wst[q] = *(const u32x4*)(src + q * 32);
+        for (int q = 0; q < NKS; ++q)
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + q * 32), (lds_ptr_t)(dst + q * kExpSlab), 16, 0, 0);
     };
-    auto wstore = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < NKS; ++q) wbuf[buf][q * SLAB + exp_swz(st_row, st_c)] = wst[q];
-    };
+    const int nchunks = p.N / kExpChunkN;
+    stage_w(0);
+    if (nchunks > 1) stage_w(1);
 
-    // ---- A fragments: row (l & 15) of each 16-row block, k = 32*ks + 8*(l>>4) .. +7 ----
+    // ---- A fragments: row (l & 15) of each 16-row block, k = 32*ks + 8*(l>>4) .. +7;
+    // k = K, K + 1 are the bias columns (1.0), k > K + 1 zero ----
     const float* X = (const float*)p.A;
     u32x4 af[RB][NKS];
 #pragma unroll
@@ -102,9 +120,10 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
                 for (int e = 0; e < 8; e += 2) {
                     // K even: pairs are wholly in or out; out-of-range pairs read pair 0
                     const bool in = k0 + e < p.K;
-                    const float2 t = *(const float2*)(row + (in ? k0 + e : 0));
-                    v[e] = in ? t.x : 0.f;
-                    v[e + 1] = in ? t.y : 0.f;
+                    const float t = k0 + e == p.K ? 1.f : 0.f;
+                    const float2 x = *(const float2*)(row + (in ? k0 + e : 0));
+                    v[e] = in ? x.x : t;
+                    v[e + 1] = in ? x.y : t;
                 }
                 af[rb][ks] = pack8<CT>(v);
             }
@@ -118,6 +137,35 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
             const int64_t off = g.seq_off[pr.x];
             const int len = g.seq_len[pr.x];
             const int f0 = pr.y - g.lead + t * p.stride;
+            // no camera concat and no clamped frame in the row (the common case): the
+            // row's K values are contiguous in the sequence, one base address per row.
+            // Only the last k-slab holds k >= K (K + 2 > 32 (NKS - 1) and K even).
+            const bool flat = g.cams == nullptr && f0 >= 0 && f0 + p.K / p.lda <= len;
+            if (__all(flat)) {
+                const float* row = g.kps + (off + f0) * g.f2;
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) {
+                    const int k0 = ks * 32 + (lane >> 4) * 8;
+                    float v[8];
+#pragma unroll
+                    for (int e = 0; e < 8; e += 2) {
+                        const int k = k0 + e;
+                        if (ks + 1 < NKS) {
+                            const float2 x = *(const float2*)(row + k);
+                            v[e] = x.x;
+                            v[e + 1] = x.y;
+                        } else {
+                            const bool in = k < p.K;
+                            const float t1 = k == p.K ? 1.f : 0.f;
+                            const float2 x = *(const float2*)(row + (in ? k : 0));
+                            v[e] = in ? x.x : t1;
+                            v[e + 1] = in ? x.y : t1;
+                        }
+                    }
+                    af[rb][ks] = pack8<CT>(v);
+                }
+                continue;
+            }
             // tap = k / lda without an integer division: k < 2^12 and lda <= 2^11, so
             // (k + 0.5) * (1 / lda) stays > 1/(4 lda) away from the next integer
             const float inv_lda = 1.0f / (float)p.lda;
@@ -130,6 +178,7 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
                     // lda, f2 and K even: a pair never straddles a tap or the kps|cams edge
                     const int k = k0 + e;
                     const bool in = k < p.K;
+                    const float t1 = k == p.K ? 1.f : 0.f;
                     const int tap = in ? (int)(((float)k + 0.5f) * inv_lda) : 0;
                     const int c = in ? k - tap * p.lda : 0;
                     int fr = f0 + tap;
@@ -137,69 +186,65 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
                     const int64_t gf = off + fr;
                     const float* src = c < g.f2 ? g.kps + gf * g.f2 + c : g.cams + gf * 12 + (c - g.f2);
                     const float2 tv = *(const float2*)src;
-                    v[e] = in ? tv.x : 0.f;
-                    v[e + 1] = in ? tv.y : 0.f;
+                    v[e] = in ? tv.x : t1;
+                    v[e + 1] = in ? tv.y : t1;
                 }
                 af[rb][ks] = pack8<CT>(v);
             }
         }
     }
+    exp_vm<0>();  // weight chunks 0 and 1 (and the A loads) landed
+    __builtin_amdgcn_s_barrier();
 
-    const int nchunks = p.N / kExpChunkN;
-    wload(0);
-    wstore(0);
-    if (nchunks > 1) wload(1);
-    __syncthreads();
-
-    const int frag_off = (lane & 15) * 4 + (((lane >> 4) + 2 * (((lane & 15) >> 2) & 3)) & 3);
+#ifdef VP3D_ABLATION
+    // measurement builds only (tools/ubench/expand_check): 2 = no global stores,
+    // 4 = no wait for the next weight chunk (results wrong; timing only)
+    const int abl = g_expand_abl;
+#else
+    constexpr int abl = 0;
+#endif
+    const int frag_off = ((lane & 15) * 4 + (((lane >> 4) + 2 * (((lane & 15) >> 2) & 3)) & 3)) * 16;
     CT* Y = (CT*)p.Y;
+    typedef short short2v __attribute__((ext_vector_type(2)));
+    // ReLU on the packed 16-bit results: max with +0 (bits 0); no ReLU: max with the
+    // smallest int16, a no-op
+    const short2v floor2 = p.relu ? short2v{0, 0} : short2v{-32768, -32768};
     for (int ch = 0; ch < nchunks; ++ch) {
-        const int buf = ch & 1;
+        // chunk ch + 2 goes to the slot chunk ch - 1 used: every wave passed the barrier
+        // that ended chunk ch - 1 after its last fragment read there
+        if (ch + 2 < nchunks) stage_w(ch + 2);
+        const char* wb = smem + (ch % kExpRing) * kChunk;
         f32x4 acc[RB][4];
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[rb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             u32x4 wf[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) wf[j] = wbuf[buf][ks * SLAB + j * 64 + frag_off];
+            for (int j = 0; j < 4; ++j) wf[j] = *(const u32x4*)(wb + ks * kExpSlab + j * 1024 + frag_off);
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[rb][j] = mfma16<CT>(wf[j], af[rb][ks], acc[rb][j]);
+                for (int j = 0; j < 4; ++j)
+                    acc[rb][j] = mfma16<CT>(wf[j], af[rb][ks], ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[rb][j]);
         }
-        // chunk ch+1 was loaded into registers during chunk ch-1; its LDS buffer was
-        // last read in chunk ch-1, which every wave finished before the barrier below
-        if (ch + 1 < nchunks) wstore(buf ^ 1);
-        if (ch + 2 < nchunks) wload(ch + 2);
 
         // epilogue: lane holds channels n0 + 16j + 4(l>>4) + r of row rb*16 + (l & 15)
         const int n0 = ch * kExpChunkN;
-        u32x4* stage = s_out[wid];
-        typedef CT ct4 __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int nl = j * 16 + (lane >> 4) * 4;  // channel within the chunk
-            const f32x4 sc = *(const f32x4*)&s_scale[n0 + nl];
-            const f32x4 sh = *(const f32x4*)&s_shift[n0 + nl];
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
-                ct4 o;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float v = __fadd_rn(__fmul_rn(acc[rb][j][r], sc[r]), sh[r]);
-                    if (p.relu) v = v > 0.f ? v : 0.f;
-                    o[r] = (CT)v;
-                }
+                const short2v l2 = __builtin_elementwise_max(
+                    __builtin_bit_cast(short2v, cvt_pk<CT>(acc[rb][j][0], acc[rb][j][1])), floor2);
+                const short2v h2 = __builtin_elementwise_max(
+                    __builtin_bit_cast(short2v, cvt_pk<CT>(acc[rb][j][2], acc[rb][j][3])), floor2);
                 const int row = rb * 16 + (lane & 15);
-                const int c16 = nl >> 3;  // 16-byte chunk (8 channels), half (nl >> 2) & 1
+                const int c16 = nl >> 3;  // 16-byte unit (8 channels), half (nl >> 2) & 1
                 // the half is swapped on rows 8-15 of each 16: the 16 lanes of a write group
                 // then cover all 32 banks (rows r and r + 8 otherwise shared them)
                 char* dst = (char*)stage + row * 128 + ((c16 ^ (row & 7)) << 4) +
                             ((((nl >> 2) & 1) ^ ((row >> 3) & 1)) << 3);
-                *(ct4*)dst = o;
+                *(uint2*)dst = uint2{__builtin_bit_cast(uint32_t, l2), __builtin_bit_cast(uint32_t, h2)};
             }
         }
         asm volatile("" ::: "memory");
@@ -211,7 +256,9 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
             u32x4 v = stage[row * 8 + (c16 ^ (row & 7))];
             if (q & 1) v = u32x4{v.z, v.w, v.x, v.y};  // rows 8-15 of 16: halves swapped
             const int m = m_wave + row;
-            if (m < p.M) {
+            if (abl == 2) {
+                asm volatile("" ::"v"(v));
+            } else if (m < p.M) {
                 u32x4* dst = (u32x4*)(Y + (int64_t)m * p.ldy + n0 + c16 * 8);
                 if constexpr (NT)
                     __builtin_nontemporal_store(v, dst);
@@ -220,7 +267,18 @@ __global__ __launch_bounds__(256) void expand_gemm_h16(ConvGemmParams p, GatherS
             }
         }
         asm volatile("" ::: "memory");
-        __syncthreads();
+        // the next chunk's weights: younger are chunk ch + 2's DMA (if issued) and this
+        // chunk's 2 * RB stores.  A wave with rows past M may skip store instructions
+        // (all lanes masked): fewer younger operations, so it drains everything instead.
+        if (ch + 1 < nchunks && abl != 4) {
+            if (m_wave + kRowsW > p.M || abl == 2)
+                exp_vm<0>();
+            else if (ch + 2 < nchunks)
+                exp_vm<NKS + 2 * RB>();
+            else
+                exp_vm<2 * RB>();
+        }
+        __builtin_amdgcn_s_barrier();
     }
 }
 
@@ -244,17 +302,29 @@ hipError_t launch_rb_nt(const ConvGemmParams& p, const GatherSrc& g, int nks, hi
 // vs 3.14-3.18 ms per step, A/B on one box).  A smaller output is left cached for the
 // next layer.
 //
-// Row blocks of 16 per wave: fewer rows per wave, fewer VGPRs and less LDS per
-// workgroup, more resident waves to hide store / input latency, but the weight sweep is
-// repeated for every workgroup.  4 where that instantiation still holds 2 waves per SIMD
-// (<= 256 VGPR + AGPR: the plain loader with K <= 128 — 250), else 2 (the gathered
-// loader's address arithmetic, or K up to 160, put RB = 4 at 280-327 registers = 1 wave
-// per SIMD).  Measured at B = 8192 (round 1): plain K = 102: RB 4 -> 0.370, 2 -> 0.406,
-// 1 -> 0.442 ms; gathered K = 138 (config 3): 4 -> 0.548, 3 -> 0.557, 2 -> 0.400 ms.
+// Row blocks of 16 per wave (RB): more rows per wave amortise each weight chunk's
+// fragment reads and the per-workgroup prologue; LDS is 3 weight chunks + RB * 8 KB of
+// output staging per workgroup, and 2 workgroups per CU need <= 80 KB.  RB = 4 for
+// K + 2 <= 128 (80 KB, 196-209 VGPRs: 2 waves per SIMD), else 2 (the camera concat,
+// K = 138: 76 KB).  Measured on the config-4 shape (B = 65,536 windows, gathered, bf16,
+// tools/ubench/expand_check): RB 4 -> 2.07 ms, 2 -> 2.25, 1 -> 2.74; the previous
+// kernel (BN in the epilogue, weights staged through VGPRs, a full drain per chunk)
+// took 3.12 ms.
+#ifdef VP3D_ABLATION
+int g_expand_rb = 0;
+#endif
 template <typename CT, bool GATHER>
 hipError_t launch_t(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     const bool nt = (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
-    if (!GATHER && nks <= 4)
+#ifdef VP3D_ABLATION
+    if (g_expand_rb == 1)
+        return nt ? launch_rb_nt<CT, 1, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 1, GATHER, false>(p, g, nks, s);
+    if (g_expand_rb == 2)
+        return nt ? launch_rb_nt<CT, 2, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 2, GATHER, false>(p, g, nks, s);
+    if (g_expand_rb == 4)
+        return nt ? launch_rb_nt<CT, 4, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 4, GATHER, false>(p, g, nks, s);
+#endif
+    if (nks <= 4)
         return nt ? launch_rb_nt<CT, 4, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 4, GATHER, false>(p, g, nks, s);
     return nt ? launch_rb_nt<CT, 2, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 2, GATHER, false>(p, g, nks, s);
 }
@@ -264,8 +334,8 @@ hipError_t launch_t(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStr
 bool expand_gemm_eligible(const ConvGemmParams& p, Act out_type, Act compute) {
     if (compute == Act::F32 || out_type != compute) return false;
     if (p.Ktap != p.K || p.dil != 1) return false;  // taps collapsed into one contiguous K run
-    const int nks = (p.K + 31) / 32;
-    if (nks < 1 || nks > 5 || nks * 32 > p.Kp) return false;  // K <= 160 (LDS for 2 WG/CU)
+    const int nks = (p.K + 2 + 31) / 32;  // K data columns + the two bias columns
+    if (nks < 1 || nks > 5 || nks * 32 > p.Kp) return false;  // K <= 158 (LDS for 2 WG/CU)
     if (p.K % 2 || p.lda % 2 || (reinterpret_cast<uintptr_t>(p.A) & 7)) return false;
     if (p.N % kExpChunkN || p.N > kExpMaxN || p.ldy % 8 || (reinterpret_cast<uintptr_t>(p.Y) & 15))
         return false;
@@ -280,7 +350,7 @@ bool expand_gather_eligible(const ConvGemmParams& p, const GatherSrc& g, Act out
 }
 
 hipError_t launch_expand_gemm(const ConvGemmParams& p, Act compute, hipStream_t stream) {
-    const int nks = (p.K + 31) / 32;
+    const int nks = (p.K + 2 + 31) / 32;
     const GatherSrc none{};
     return compute == Act::BF16 ? launch_t<bf16, false>(p, none, nks, stream)
                                 : launch_t<f16, false>(p, none, nks, stream);
@@ -288,8 +358,15 @@ hipError_t launch_expand_gemm(const ConvGemmParams& p, Act compute, hipStream_t 
 
 hipError_t launch_expand_gemm_gather(const ConvGemmParams& p, const GatherSrc& g, Act compute,
                                      hipStream_t stream) {
-    const int nks = (p.K + 31) / 32;
+    const int nks = (p.K + 2 + 31) / 32;
     return compute == Act::BF16 ? launch_t<bf16, true>(p, g, nks, stream) : launch_t<f16, true>(p, g, nks, stream);
 }
 
 }  // namespace vp3d
+
+#ifdef VP3D_ABLATION
+namespace vp3d {
+hipError_t expand_gemm_set_ablation(int a) { return hipMemcpyToSymbol(HIP_SYMBOL(g_expand_abl), &a, sizeof(int)); }
+void expand_gemm_set_rb(int rb) { g_expand_rb = rb; }
+}  // namespace vp3d
+#endif

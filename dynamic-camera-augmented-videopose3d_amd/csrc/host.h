@@ -40,6 +40,19 @@ inline uint16_t f32_to_f16_rne(float f) {
     return r;
 }
 
+inline float bf16_to_f32(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+inline float f16_to_f32(uint16_t h) {
+    _Float16 v;
+    std::memcpy(&v, &h, 2);
+    return (float)v;
+}
+
 // One convolution of the stack (expand, k-conv / 1x1 of each block, shrink).
 struct Layer {
     int cin = 0, cout = 0, taps = 1, dil = 1, stride = 1;  // conv geometry
@@ -52,6 +65,11 @@ struct Layer {
     uint16_t* wh = nullptr;
     float* scale = nullptr;
     float* shift = nullptr;
+    // expand conv only (expand_gemm.hip): 16-bit weights with the BN folded in --
+    // W * scale rounded once, shift as two 16-bit columns hi + lo at k = K, K + 1 (the
+    // kernel's loader feeds them 1.0); null when K + 2 does not fit in Kp
+    uint16_t* wfbf = nullptr;
+    uint16_t* wfh = nullptr;
 };
 
 struct ProfEvent {

@@ -163,9 +163,12 @@ void free_layers(vp3d_handle* h) {
         hipFree(L.wh);
         hipFree(L.scale);
         hipFree(L.shift);
+        hipFree(L.wfbf);
+        hipFree(L.wfh);
         L.w32 = nullptr;
         L.wbf = L.wh = nullptr;
         L.scale = L.shift = nullptr;
+        L.wfbf = L.wfh = nullptr;
     }
 }
 
@@ -225,6 +228,28 @@ int upload_weights(vp3d_handle* h, const float* const* w, int n) {
         HIP_TRY(hipMemcpy(L.wh, ph.data(), ph.size() * 2, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(L.scale, sc.data(), L.cout * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(L.shift, shv.data(), L.cout * 4, hipMemcpyHostToDevice));
+        if (li == 0 && !is_shrink && L.K + 2 <= L.Kp) {
+            // the expand conv's BN-folded 16-bit copy (expand_gemm.hip)
+            std::vector<uint16_t> fbf(p32.size(), 0), fh(p32.size(), 0);
+            for (int o = 0; o < L.cout; ++o) {
+                for (int k = 0; k < L.K; ++k) {
+                    const float v = p32[(size_t)o * L.Kp + k] * sc[o];
+                    fbf[(size_t)o * L.Kp + k] = f32_to_bf16_rne(v);
+                    fh[(size_t)o * L.Kp + k] = f32_to_f16_rne(v);
+                }
+                const uint16_t hb = f32_to_bf16_rne(shv[o]), hh = f32_to_f16_rne(shv[o]);
+                fbf[(size_t)o * L.Kp + L.K] = hb;
+                fh[(size_t)o * L.Kp + L.K] = hh;
+                fbf[(size_t)o * L.Kp + L.K + 1] = f32_to_bf16_rne(shv[o] - bf16_to_f32(hb));
+                fh[(size_t)o * L.Kp + L.K + 1] = f32_to_f16_rne(shv[o] - f16_to_f32(hh));
+            }
+            if (!L.wfbf) {
+                HIP_TRY(hipMalloc(&L.wfbf, fbf.size() * 2));
+                HIP_TRY(hipMalloc(&L.wfh, fh.size() * 2));
+            }
+            HIP_TRY(hipMemcpy(L.wfbf, fbf.data(), fbf.size() * 2, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(L.wfh, fh.data(), fh.size() * 2, hipMemcpyHostToDevice));
+        }
     }
     return VP3D_OK;
 }
@@ -493,9 +518,13 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         const Act o_type = last ? Act::F32 : act;
         hipError_t e = hipSuccess;
         bool launched = false;
-        if (first && gs && act != Act::F32 && expand_gather_eligible(p, *gs, o_type, act)) {
+        // the expand kernel takes the BN-folded weights (Layer::wfbf / wfh)
+        const void* wfold = act == Act::BF16 ? (const void*)L.wfbf : (const void*)L.wfh;
+        ConvGemmParams pf = p;
+        pf.W = wfold;
+        if (first && gs && act != Act::F32 && wfold && expand_gather_eligible(pf, *gs, o_type, act)) {
             // the window gather (+ camera concat) fused into the expand conv's operand loads
-            e = launch_expand_gemm_gather(p, *gs, act, s);
+            e = launch_expand_gemm_gather(pf, *gs, act, s);
             launched = true;
         } else if (first && gs) {
             // any other first-layer path: gather the windows into the scratch tensor first
@@ -514,9 +543,10 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
             p.A = x;
         }
         if (launched) {
-        } else if (first && act != Act::F32 && expand_gemm_eligible(p, o_type, act)) {
+        } else if (first && act != Act::F32 && wfold && expand_gemm_eligible(pf, o_type, act)) {
             // 16-bit expand conv straight from the f32 input rows (expand_gemm.hip)
-            e = launch_expand_gemm(p, act, s);
+            pf.A = p.A;
+            e = launch_expand_gemm(pf, act, s);
             launched = true;
         } else if (first && act != Act::F32) {
             // 16-bit path for the shapes expand_gemm does not take (K > 160: filter width 5
