@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--sweep", type=lambda v: [int(t) for t in v.split(",") if t], default=[1024, 8192, 65536],
                     help="config-2 batch sweep on one GPU (windows per step)")
     ap.add_argument("--no-extras", action="store_true", help="skip the fp32 leg, the sweep and the CPU baseline")
+    ap.add_argument("--pregathered", action="store_true",
+                    help="configs 2/4: time the forward over a window tensor gathered once before the "
+                         "timed region (the reference's form: batch built outside the model) instead of "
+                         "the batch assembly + forward of the default step")
     ap.add_argument("--traj", action="store_true",
                     help="config 3: camera-trajectory conditioned input (46 ch) with the "
                          "on-device window gather inside the timed step")
@@ -643,8 +647,8 @@ def windows_main(args, world, rank, dev):
     lifter.reserve(B, RF, dtype)
     y = torch.empty((B, 1, JOINTS, 3), device=dev)
     x = None
-    if not traj:
-        # the rank's shard of the global window set, gathered on device and resident
+    if not traj and args.pregathered:
+        # the rank's shard of the global window set, gathered once on device and resident
         x = pool.seqs.gather(pairs, RF, pad, "2d").view(B, RF, jin, 2)
 
     def make_step(dt_, x_, pairs_, y_):
@@ -654,6 +658,13 @@ def windows_main(args, world, rank, dev):
                 # into the expand conv's operand loads, then the stack
                 pool.seqs.refresh_cameras()
                 lifter.forward_windows(pool.seqs, pairs_, RF, pad, concat_cams=True, dtype=dt_, out=y_)
+        elif x_ is None:
+            def step():
+                # configs 2/4: the batch of the step (ChunkedGenerator's window gather with
+                # edge clamping, generators.py:102-137) assembled on device from the resident
+                # sequences -- fused into the expand conv's operand loads on the 16-bit path --
+                # then the stack (TemporalModel.py:62-76)
+                lifter.forward_windows(pool.seqs, pairs_, RF, pad, concat_cams=False, dtype=dt_, out=y_)
         else:
             def step():
                 lifter.forward(x_, dt_, out=y_)
@@ -703,7 +714,9 @@ def windows_main(args, world, rank, dev):
         "config": {
             "workload": ("config3 trajectory-conditioned (46ch) " if traj else
                          ("config4 global batch sharded over ranks, " if scaling == "strong" else "config2 ")
-                         ) + "TemporalModelOptimized1f 243-frame RF windows, 17 joints, 1024 ch",
+                         ) + "TemporalModelOptimized1f 243-frame RF windows, 17 joints, 1024 ch" +
+                        ("; windows pre-gathered before the timed region" if x is not None else
+                         "; window batch assembled on device from resident sequences inside the step"),
             "global_batch": G, "windows_per_gpu": B,
             "parallelism": f"dp{world} (contiguous shards of one global window set, no collective)"
             if scaling == "strong" else f"dp{world} (independent windows per rank, no collective)",
@@ -740,7 +753,7 @@ def windows_main(args, world, rank, dev):
                         sweep[str(Bs)] = round(value, 2)
                         continue
                     ps = torch.from_numpy(pool.global_pairs(Bs)).to(dev)
-                    xsw = pool.seqs.gather(ps, RF, pad, "2d").view(Bs, RF, jin, 2)
+                    xsw = pool.seqs.gather(ps, RF, pad, "2d").view(Bs, RF, jin, 2) if args.pregathered else None
                     ysw = torch.empty((Bs, 1, JOINTS, 3), device=dev)
                     lifter.reserve(Bs, RF, dtype)
                     ks = max(5, args.steps // 2)

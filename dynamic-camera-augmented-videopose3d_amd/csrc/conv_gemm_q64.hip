@@ -228,12 +228,18 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
     }
     if (wr == 0) qbarrier();  // match group 1's extra barrier
 
-    const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(p.Y, (uint32_t)((size_t)p.M * p.ldy * sizeof(CT)));
+    // the output resource starts at the tile's first row (outputs past 2^31 bytes: the
+    // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
+    const size_t y_rest = (size_t)(p.M - m0) * p.ldy * sizeof(CT);
+    const __amdgpu_buffer_rsrc_t y_rsrc =
+        make_rsrc((const CT*)p.Y + (size_t)m0 * p.ldy, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
     // the residual (1x1 convs) is loaded inside the epilogue, one row block ahead of its use
     if (p.R)
-        epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc);
+        epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc,
+                                        nullptr, m0);
     else
-        epilogue_tp<CT, 8, false, 0, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc);
+        epilogue_tp<CT, 8, false, 0, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc,
+                                        nullptr, m0);
 }
 
 }  // namespace
@@ -245,9 +251,9 @@ bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, A
     if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
         (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
         return false;
-    if ((size_t)p.M * p.ldy * 2 >= (1u << 31)) return false;  // 32-bit buffer offsets
-    if (p.R && (size_t)((p.M + p.T_out - 1) / p.T_out) * p.R_T * p.ldr * 2 >= (1u << 31)) return false;
-    return true;
+    // any output size: the store resource is rebased per tile, A / W / residual
+    // addresses are 64-bit (A rows and Np * Kp stay below 2^31)
+    return (size_t)p.N * p.Kp < (1u << 31);
 }
 
 hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream) {

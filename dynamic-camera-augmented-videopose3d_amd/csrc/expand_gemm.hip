@@ -42,7 +42,6 @@ constexpr int kExpChunkN = 64;  // output channels per chunk
 constexpr int kExpMaxN = 1024;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
-constexpr int kExpRing = 3;     // weight chunks resident (current, next, next-but-one)
 constexpr int kExpSlab = 4096;  // bytes of one [64 channels][32 k] slab
 #ifdef VP3D_ABLATION
 __device__ int g_expand_abl;
@@ -72,27 +71,28 @@ __device__ __forceinline__ void exp_vm() {
 // reads (row l & 15 of a 16-row block, k-chunk l >> 4) are bank-conflict free.  The DMA
 // writes a slab lane-linearly (wave w: rows 16w .. 16w + 15); the permutation is applied
 // to the global source address.
-template <typename CT, int NKS, int RB, bool GATHER, bool NT = false>
+// RING: weight chunks resident (3: current, next, next-but-one; 2: current, next)
+template <typename CT, int NKS, int RB, bool GATHER, bool NT = false, int RING = 3>
 __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
     constexpr int kRowsW = 16 * RB;
     constexpr int kRows = kRowsW * kExpWaves;
     constexpr int kChunk = NKS * kExpSlab;
     // ring of weight chunks, then per-wave output staging: kRowsW rows x 128 B, 16-byte
     // unit c of row r at c ^ (r & 7)
-    __shared__ __attribute__((aligned(16))) char smem[kExpRing * kChunk + kExpWaves * kRowsW * 128];
+    __shared__ __attribute__((aligned(16))) char smem[RING * kChunk + kExpWaves * kRowsW * 128];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int m_wave = blockIdx.x * kRows + wid * kRowsW;
-    u32x4* const stage = (u32x4*)(smem + kExpRing * kChunk + wid * kRowsW * 128);
+    u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * 128);
 
     // ---- weight chunk DMA: NKS pieces of 1 KB per wave ----
     const int dr = 16 * wid + (lane >> 2);
     const int dc = ((lane & 3) - 2 * ((dr >> 2) & 3)) & 3;
     const CT* const wsrc = (const CT*)p.W + (int64_t)dr * p.Kp + dc * 8;
     auto stage_w = [&](int chunk) {
-        char* dst = smem + (chunk % kExpRing) * kChunk + wid * 1024;
+        char* dst = smem + (chunk % RING) * kChunk + wid * 1024;
         const CT* src = wsrc + (int64_t)chunk * kExpChunkN * p.Kp;
 #pragma unroll
         for (int q = 0; q < NKS; ++q)
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     };
     const int nchunks = p.N / kExpChunkN;
     stage_w(0);
-    if (nchunks > 1) stage_w(1);
+    if (RING == 3 && nchunks > 1) stage_w(1);
 
     // ---- A fragments: row (l & 15) of each 16-row block, k = 32*ks + 8*(l>>4) .. +7;
     // k = K, K + 1 are the bias columns (1.0), k > K + 1 zero ----
@@ -212,8 +212,8 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     for (int ch = 0; ch < nchunks; ++ch) {
         // chunk ch + 2 goes to the slot chunk ch - 1 used: every wave passed the barrier
         // that ended chunk ch - 1 after its last fragment read there
-        if (ch + 2 < nchunks) stage_w(ch + 2);
-        const char* wb = smem + (ch % kExpRing) * kChunk;
+        if (ch + RING - 1 < nchunks) stage_w(ch + RING - 1);
+        const char* wb = smem + (ch % RING) * kChunk;
         f32x4 acc[RB][4];
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
         if (ch + 1 < nchunks && abl != 4) {
             if (m_wave + kRowsW > p.M || abl == 2)
                 exp_vm<0>();
-            else if (ch + 2 < nchunks)
+            else if (RING == 3 && ch + 2 < nchunks)
                 exp_vm<NKS + 2 * RB>();
             else
                 exp_vm<2 * RB>();
@@ -282,15 +282,15 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     }
 }
 
-template <typename CT, int RB, bool GATHER, bool NT>
+template <typename CT, int RB, bool GATHER, bool NT, int RING = 3>
 hipError_t launch_rb_nt(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     const dim3 grid((p.M + 64 * RB - 1) / (64 * RB));
     switch (nks) {
-        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
-        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
-        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
-        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
-        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB, GATHER, NT>), grid, dim3(256), 0, s, p, g); break;
+        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
+        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
+        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
+        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
+        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -317,6 +317,10 @@ template <typename CT, bool GATHER>
 hipError_t launch_t(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     const bool nt = (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
 #ifdef VP3D_ABLATION
+    if (g_expand_rb == 12)  // RB 2, double-buffered weights (3 workgroups per CU)
+        return nt ? launch_rb_nt<CT, 2, GATHER, true, 2>(p, g, nks, s) : launch_rb_nt<CT, 2, GATHER, false, 2>(p, g, nks, s);
+    if (g_expand_rb == 14)  // RB 4, double-buffered weights
+        return nt ? launch_rb_nt<CT, 4, GATHER, true, 2>(p, g, nks, s) : launch_rb_nt<CT, 4, GATHER, false, 2>(p, g, nks, s);
     if (g_expand_rb == 1)
         return nt ? launch_rb_nt<CT, 1, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 1, GATHER, false>(p, g, nks, s);
     if (g_expand_rb == 2)

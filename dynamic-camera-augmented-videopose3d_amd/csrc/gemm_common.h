@@ -314,10 +314,13 @@ __device__ __forceinline__ void load_residual_tp_buf(const ConvGemmParams& p, u3
 // HAS_R: -1 = p.R decides at run time; 0 / 1 = known at compile time (straight-line
 // code, so the compiler's own vmcnt waits before the residual uses stay counted).
 // AUX: cache policy of the output stores (0 = default; 2 = nt, streamed past the caches)
+// m_base: the row y_rsrc starts at (callers with outputs past 2^31 bytes rebase the
+// resource per tile; store offsets are then tile-relative)
 template <typename CT, int MI, bool PRE = false, int HAS_R = -1, int AUX = 0>
 __device__ __forceinline__ void epilogue_tp(const ConvGemmParams& p, f32x4 (&acc)[MI][4], int mw, int nw,
                                             int lane, const float* s_scale, const float* s_shift,
-                                            __amdgpu_buffer_rsrc_t y_rsrc, const u32x4 (*pre)[2] = nullptr) {
+                                            __amdgpu_buffer_rsrc_t y_rsrc, const u32x4 (*pre)[2] = nullptr,
+                                            int m_base = 0) {
     const int grp = lane >> 4;
     const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
     float sc[4][4], sh[4][4];
@@ -382,7 +385,7 @@ __device__ __forceinline__ void epilogue_tp(const ConvGemmParams& p, f32x4 (&acc
             ct8 o;
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = (CT)v[e];
-            const uint32_t yo = m < p.M ? (uint32_t)(((size_t)m * p.ldy + nw + 32 * jp + c0) * sizeof(CT))
+            const uint32_t yo = m < p.M ? (uint32_t)(((size_t)(m - m_base) * p.ldy + nw + 32 * jp + c0) * sizeof(CT))
                                         : 0xFFFFFFF0u;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), y_rsrc, yo, 0, AUX);
         }

@@ -74,6 +74,27 @@ def test_opt1f_243_h16_large_batch(dtype):
     _check(y, ref, gt, dtype)
 
 
+def test_opt1f_outputs_past_2gb_bf16():
+    """B = 40,000 windows: the block-1 outputs are 2.2 GB (past 2^31 bytes: the q64
+    kernel's per-tile output resource) and the expand output 6.6 GB.  The input is 64
+    distinct windows tiled 625 times, so every output window is checked against the
+    oracle (windows are independent in the strided model)."""
+    model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024, seed=0)
+    xs = synth.normalized_windows(1, "x64_243", 64, 243)
+    ref = lifter_forward(sd, xs, [3, 3, 3, 3, 3], strided=True).numpy()
+    x = np.ascontiguousarray(np.tile(xs, (625, 1, 1, 1)))
+    model.cuda().set_compute_dtype("bf16")
+    with torch.no_grad():
+        y = model(torch.from_numpy(x).cuda())
+    torch.cuda.synchronize()
+    y = y.cpu().numpy().reshape((625,) + ref.shape)
+    del x
+    gt = synth.gt_poses(3, "gt", 64 * ref.shape[1], 17).reshape(ref.shape)
+    for r in (0, 1, 311, 623, 624):  # first, middle and last copies (last tiles of every layer)
+        _check(y[r], ref, gt, "bf16")
+    assert np.abs(y - ref[None]).max() <= H16_TOL["bf16"][0]
+
+
 @pytest.mark.parametrize("gemm,opt1f", [("big", True), ("8p", True), ("8p", False), ("q64", False)])
 def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
     """Every 256x256 kernel on the shapes the default dispatch gives another one:

@@ -6,8 +6,8 @@
 Reads the FETCH_SIZE and WRITE_SIZE passes (`tools/pmc_pass.sh TAG FETCH_SIZE WRITE_SIZE`
 over a `bench.py` run), orders the dispatches by Dispatch_Id and splits them into
 forwards: a forward starts at the expand-conv dispatch of the bench batch (grid =
-ceil(B*81/256) workgroups of 256 threads for the fused expand kernel, or the
-pack-rows kernel of the older path) and is followed by the 9 conv-GEMM dispatches
+ceil(B*81/256) or ceil(B*81/128) workgroups of 256 threads for the fused expand
+kernel) and is followed by the 9 conv-GEMM dispatches
 of blocks 1-4 and the shrink, in layer order.
 
 Units and corrections (MI355X_MICROARCH.md, "HBM"): FETCH_SIZE and WRITE_SIZE
@@ -25,9 +25,9 @@ LAYERS = ["expand", "block1_k3", "block1_1x1", "block2_k3", "block2_1x1", "block
           "block3_1x1", "block4_k3", "block4_1x1", "shrink"]
 
 
-def read_counter(d, name):
+def read_counter(d, name, prefix="pmc"):
     rows = {}
-    for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(d, prefix + "*", "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 if r["Counter_Name"] != name:
@@ -39,11 +39,13 @@ def read_counter(d, name):
 def forwards(rows, B):
     """Yield lists of (layer, value) per forward of batch B."""
     ids = sorted(rows)
-    expand_grid = ((B * 81 + 255) // 256) * 256
+    # the fused expand kernel runs 256 rows per workgroup (RB = 4) or 128 (RB = 2, the
+    # camera concat): grid in threads = workgroups x 256
+    expand_grids = {((B * 81 + 255) // 256) * 256, ((B * 81 + 127) // 128) * 256}
     i = 0
     while i < len(ids):
         name, grid, _ = rows[ids[i]]
-        start = ("expand_gemm" in name and grid == expand_grid)
+        start = ("expand_gemm" in name and grid in expand_grids)
         if not start:
             i += 1
             continue
@@ -66,10 +68,11 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--dominant", default="block1_k3")
     ap.add_argument("--out")
+    ap.add_argument("--prefix", default="pmc", help="PMC pass directories under DIR (pmc*, traj_pmc*)")
     a = ap.parse_args()
     acc = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
     for c in acc:
-        for seq in forwards(read_counter(a.dir, c), a.batch):
+        for seq in forwards(read_counter(a.dir, c, a.prefix), a.batch):
             for layer, v in seq:
                 acc[c][layer].append(v)
     per_layer = {}
@@ -84,7 +87,7 @@ def main():
     out = {"batch": a.batch, "dtype": a.dtype, "dominant": a.dominant,
            "hbm_bytes_per_launch": per_layer.get(a.dominant, {}).get("hbm_bytes"),
            "per_layer": per_layer,
-           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in {a.dir}; "
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in {a.dir}/{a.prefix}*; "
                      "FETCH_SIZE x 2 (gfx950 128-B requests tallied as 64 B), KiB -> B"}
     s = json.dumps(out, indent=1)
     print(s)
