@@ -59,7 +59,9 @@ __device__ __forceinline__ void qvm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename CT>
+// EPI (measurement builds only, tools/ubench/gemm_check with VP3D_ABL): 0 = the epilogue,
+// 1 = stores issued but dropped by the range check (no output traffic), 2 = no epilogue
+template <typename CT, int EPI = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
     __shared__ __attribute__((aligned(16))) char smem[2 * QBUF + 2 * QMAXN * 4];
     float* const s_scale = (float*)(smem + 2 * QBUF);
@@ -232,8 +234,18 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
     // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
     const size_t y_rest = (size_t)(p.M - m0) * p.ldy * sizeof(CT);
     const __amdgpu_buffer_rsrc_t y_rsrc =
-        make_rsrc((const CT*)p.Y + (size_t)m0 * p.ldy, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
-    // the residual (1x1 convs) is loaded inside the epilogue, one row block ahead of its use
+        make_rsrc((const CT*)p.Y + (size_t)m0 * p.ldy,
+                  EPI == 1 ? 0u : (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+    if (EPI == 2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+    }
+    // the residual (1x1 convs) is loaded inside the epilogue, one row block ahead of its
+    // use (issuing all 16 loads of the block when the K loop ends measured the same:
+    // block-1 1x1 + residual 0.674 vs 0.667 ms -- per-CU bandwidth, not latency)
     if (p.R)
         epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc,
                                         nullptr, m0);
@@ -258,6 +270,17 @@ bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, A
 
 hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream) {
     const dim3 grid(((p.M + QM - 1) / QM) * (p.N / QN));
+#ifdef VP3D_ABLATION
+    static const int abl = [] {
+        const char* e = getenv("VP3D_ABL");
+        return e ? atoi(e) : 0;
+    }();
+    if (compute == Act::BF16 && (abl == 1 || abl == 2)) {
+        if (abl == 1) hipLaunchKernelGGL((conv_gemm_q64<__bf16, 1>), grid, dim3(512), 0, stream, p);
+        else hipLaunchKernelGGL((conv_gemm_q64<__bf16, 2>), grid, dim3(512), 0, stream, p);
+        return hipGetLastError();
+    }
+#endif
     if (compute == Act::BF16)
         hipLaunchKernelGGL((conv_gemm_q64<__bf16>), grid, dim3(512), 0, stream, p);
     else
