@@ -99,8 +99,10 @@ def synth_windows(B, T, jin, seed, device):
 
 def stream_main(args, world, rank, dev):
     """Config 5: causal TemporalModel, one frame in / one pose out per step.  16-bit
-    weights: a graph of Q steps is ONE persistent launch (weights resident in LDS across
-    the 256 CUs, 9 in-launch hand-offs per step); fp32: 10 GEMV launches per step."""
+    weights: a graph of Q steps is ONE persistent launch -- by default the layer-pipelined
+    form (each CU runs one layer with its weights in VGPRs, the frames of the graph flow
+    through the layer groups; VP3D_STREAM_MODE=persist: every CU runs every layer with its
+    weights in LDS); fp32: 10 GEMV launches per step."""
     from common.models.TemporalModel import TemporalModel
     from oracle.temporal_ref import lifter_forward
     from vp3d_amd import synth
@@ -118,7 +120,7 @@ def stream_main(args, world, rank, dev):
     # a synthetic clip fills the device frame queue; every step reads its own slot
     fq.copy_(synth_windows(1, Q, JOINTS, 1000 + rank, dev)[0].reshape(Q, -1))
     st.capture(s, steps=G)
-    mode = "persistent" if st.persistent else "launches"
+    mode = st.mode
     n_launch = max(1, -(-args.steps // G))
     n_warm = max(1, -(-args.warmup // G))
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -192,11 +194,13 @@ def stream_main(args, world, rank, dev):
         "config": {"workload": "config5 causal streaming TemporalModel 243-frame RF, 17 joints, "
                                "1024 ch, one frame per step, hipGraph of "
                                f"{G} consecutive steps fed from the device frame queue"
-                               + (" (one persistent launch: weights resident in LDS)" if mode == "persistent"
-                                  else " (10 GEMV launches per step)"),
+                               + {"pipe": " (one persistent launch, one layer per CU with its weights in VGPRs, "
+                                          "frames pipelined through the layer groups)",
+                                  "persist": " (one persistent launch: every CU runs every layer, weights in LDS)",
+                                  "launches": " (10 GEMV launches per step)"}[mode],
                    "frames_per_step": 1, "steps_per_graph": G, "mode": mode, "parallelism": f"replicas{world}"},
-        "roofline": {"bound": "hbm", "kernel": ("stream_persist_kernel" if mode == "persistent"
-                                                else "stream step (10 stream_gemv launches)"),
+        "roofline": {"bound": "hbm", "kernel": {"pipe": "stream_pipe_kernel", "persist": "stream_persist_kernel",
+                                                "launches": "stream step (10 stream_gemv launches)"}[mode],
                      "note": "achieved = the step's weight bytes / step time (the unit of work of a "
                              "weight-streaming step; in the persistent form the weights stay in LDS)",
                      "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",

@@ -134,6 +134,39 @@ struct StreamPersistParams {
 int stream_persist_lds_bytes();
 hipError_t launch_stream_persist(const StreamPersistParams& p, Act wtype, hipStream_t s);
 
+// Causal streaming, layer-pipelined form (stream_pipe.hip): workgroup g runs ONE layer
+// ("role" l = layer index: 0 expand, 2b-1 / 2b block b's k-conv / 1x1, nl-1 shrink) for
+// the channels [N_l * i / n_l, N_l * (i+1) / n_l) of its role (i = g - cu0[l], n_l =
+// cu0[l+1] - cu0[l]) with their 16-bit weights in VGPRs; layer outputs go to the next
+// role's workgroups through {tag = frame + 1, value} granules, slot frame % queue.
+constexpr int kPipeCwK = 3;        // k-conv rows per wave (3 taps each)
+constexpr int kPipeCwP = 8;        // 1x1 / shrink rows per wave
+constexpr int kPipeMaxCh = 512;    // channels per workgroup (expand: one per lane of 8 waves)
+constexpr int kPipeExpandK = 128;  // expand K (3 frames x J_in*F, zero-padded)
+struct StreamPipeParams {
+    const void* W[kStreamMaxLayers];       // packed 16-bit weights [Np][Kp], tap-major K
+    const float* scale[kStreamMaxLayers];  // folded BatchNorm (shrink: 1 / bias)
+    const float* shift[kStreamMaxLayers];
+    int Kp[kStreamMaxLayers], N[kStreamMaxLayers];
+    int cu0[kStreamMaxLayers + 1];         // role l owns workgroups [cu0[l], cu0[l+1])
+    int nl, nb, C, cin0;
+    int dil[kStreamMaxBlocks + 1], ring[kStreamMaxBlocks + 1];  // per block b >= 1 (ring: pow2 >= 2d+1)
+    const float* frames;                   // frame queue (queue slots of cin0 floats)
+    int queue;                             // power of two
+    float* poses;                          // pose ring (queue slots of N[nl-1] floats)
+    int* frames_seen;                      // stream position (read at start, advanced by the last workgroup)
+    unsigned* arrivals;                    // end-of-launch arrival counter (zero between launches)
+    unsigned long long* gran;              // [queue][2nb+1 edges][C] granules
+    unsigned* err;                         // sticky timeout word
+    float* state;                          // [workgroups][state_stride]: k-conv rings / expand history
+    int state_stride;
+    int steps;
+};
+int stream_pipe_lds_bytes(int C, int cin0, int max_ring);
+bool stream_pipe_channels_ok(int C);
+hipError_t stream_pipe_prepare(Act wtype, int C, int lds_bytes);  // dynamic-LDS attribute, once
+hipError_t launch_stream_pipe(const StreamPipeParams& p, Act wtype, int lds_bytes, hipStream_t s);
+
 // preprocess kernels (preprocess.hip)
 hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, float* out,
                                    bool inverse, hipStream_t s);

@@ -1,0 +1,474 @@
+// Causal streaming step as ONE layer-pipelined persistent launch per batch of frames
+// (BASELINE config 5, 16-bit weights).
+//
+// Model: the causal dilated TemporalModel (reference common/models/TemporalModel.py:79-138,
+// causal=True: block b's residual is the newest frame of its input, :132; output t of a
+// k-conv reads its input at times t - 2d, t - d, t, clamped at 0 -- the 2*pad copies of
+// frame 0 that UnchunkedGenerator puts in front of a causal sequence, generators.py:193-198).
+//
+// Why another form (stream_persist.hip spreads every layer over all 256 CUs): there, each
+// of the 9 layer outputs of a step is an all-to-all edge read by all 256 CUs, ~2.5 us each
+// (MI355X_MICROARCH.md "allgather"), and a step cannot start before the previous one has
+// left the last layer.  Here every workgroup (one per CU) owns ONE layer -- its "role":
+// expand, block b's k-conv, block b's 1x1 conv, or the shrink -- and a slice of that
+// layer's output channels, with the slice's 16-bit weights resident in VGPRs for the whole
+// launch.  A layer output is then read only by the next layer's group (46 / 16 CUs at 1024
+// channels instead of 256), and the groups form a pipeline over the frames of the batch:
+// while block 4 works on frame t, block 1 already works on frame t + 3.  Results are the
+// same as one frame at a time (no group reads anything a later frame writes).
+//
+// Hand-off: 8-byte {tag, value} granules (R2 of cdna_hip_programming.md Guideline 16:
+// write-through agent-scope stores, relaxed agent-scope polls); tag = absolute frame
+// index + 1, one granule slot per (frame % queue, edge, channel), so no per-launch zeroing
+// (vp3d_stream_reset clears them) and no producer can lap a consumer inside a launch.
+//
+// Layouts (one wave = 64 lanes):
+//   * k-conv / 1x1 / shrink ("k-sliced"): lane L holds elements [L*KS, L*KS + KS) of every
+//     weight row the wave owns (KS = C / 64); a channel's dot product is a lane-partial sum
+//     reduced across the wave (DPP within 16-lane rows, then the 4 row sums).
+//   * expand ("lane per channel"): lane L owns one output channel and its whole weight row
+//     (K = 3 * 34 = 102, padded to 128); the 3-frame input vector is an LDS broadcast.
+// f16 weights feed v_fma_mix_f32 (f16 x f32 + f32, exact widening); activations stay f32.
+//
+// Block b's k-conv is split by tap (as in stream_persist.hip): the newest tap completes
+// output t; the older taps' products of x(t) go into a wave-private ring of partial sums
+// for outputs t + d and t + 2d, off the critical path.  Every spin is bounded (~0.25 s of
+// the 100 MHz clock); a timeout sets the sticky error word and the workgroup leaves.
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace vp3d {
+namespace {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+constexpr int kThreads = 512;
+constexpr int kWaves = kThreads / 64;
+constexpr unsigned long long kSpinTicks = 25000000ull;  // 0.25 s of the 100 MHz clock
+
+// 16-bit weight halves of a packed u32 -> f32 (exact)
+template <typename WT>
+__device__ __forceinline__ float lo16(uint32_t w) {
+    return (float)__builtin_bit_cast(WT, (unsigned short)(w & 0xffffu));
+}
+template <typename WT>
+__device__ __forceinline__ float hi16(uint32_t w) {
+    return (float)__builtin_bit_cast(WT, (unsigned short)(w >> 16));
+}
+
+// Sum over the 64 lanes, wave-uniform result.  Within each 16-lane row: xor 1, xor 2
+// (quad_perm), half-mirror, mirror; then the four row sums in a fixed order.
+__device__ __forceinline__ float wave_sum_uniform(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return (r0 + r1) + (r2 + r3);
+}
+
+__device__ __forceinline__ void publish(gu64* g, unsigned tag, float v) {
+    const unsigned long long x = ((unsigned long long)tag << 32) | __float_as_uint(v);
+    __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Poll granules [c_lo, c_hi) of one edge slot into x (LDS); every thread owns granules
+// c_lo + tid + j * kThreads (four in flight per pass).  False on timeout (sets the error
+// word and the workgroup's abort flag) or when another wave already aborted.
+__device__ bool sweep(const gu64* g, int c_lo, int c_hi, unsigned tag, float* x, volatile int* abort_flag,
+                      unsigned* err, int tid) {
+    const unsigned long long start = __builtin_amdgcn_s_memrealtime();
+    for (int i0 = c_lo + tid; i0 < c_hi; i0 += 4 * kThreads) {
+        unsigned pending = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (i0 + j * kThreads < c_hi) pending |= 1u << j;
+        for (;;) {
+            unsigned long long v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int i = i0 + j * kThreads < c_hi ? i0 + j * kThreads : c_hi - 1;
+                v[j] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (((pending >> j) & 1u) && (unsigned)(v[j] >> 32) == tag) {
+                    x[i0 + j * kThreads - c_lo] = __uint_as_float((unsigned)v[j]);
+                    pending &= ~(1u << j);
+                }
+            if (!pending) break;
+            if (*abort_flag) return false;
+            if (__builtin_amdgcn_s_memrealtime() - start > kSpinTicks) {
+                *abort_flag = 1;
+                __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return true;
+}
+
+// Lane-partial dot products of the wave's CW rows (NT taps each) with the lane's KS
+// input elements xl: s[tap][j] = sum_i w[tap][j][i] * xl[i].
+template <typename WT, int NT, int CW, int KS>
+__device__ __forceinline__ void lane_dots(const uint32_t (&w)[NT][CW][KS / 2], const float (&xl)[KS], int tap,
+                                          float (&s)[CW]) {
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < KS / 2; ++i) {
+            a = __builtin_fmaf(lo16<WT>(w[tap][j][i]), xl[2 * i], a);
+            a = __builtin_fmaf(hi16<WT>(w[tap][j][i]), xl[2 * i + 1], a);
+        }
+        s[j] = a;
+    }
+}
+
+// Load the wave's rows of one layer into registers: row c = c_lo + wid + kWaves * j, tap
+// segment [tap * C + lane * KS, +KS) of the [Np][Kp] 16-bit matrix (rows past c_hi: zero).
+template <typename WT, int NT, int CW, int KS>
+__device__ __forceinline__ void load_rows(uint32_t (&w)[NT][CW][KS / 2], const WT* W, int Kp, int C, int c_lo,
+                                          int c_hi, int wid, int lane, int taps) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+            const int c = c_lo + wid + kWaves * j;
+#pragma unroll
+            for (int i = 0; i < KS / 2; ++i) w[t][j][i] = 0u;
+            if (c < c_hi && t < taps) {
+                const uint32_t* src = (const uint32_t*)(W + (int64_t)c * Kp + t * C + lane * KS);
+#pragma unroll
+                for (int i = 0; i < KS / 2; ++i) w[t][j][i] = src[i];
+            }
+        }
+}
+
+template <int KS>
+__device__ __forceinline__ void load_x(float (&xl)[KS], const float* x, int lane) {
+#pragma unroll
+    for (int i = 0; i < KS; i += 4) {
+        const float4 v = *(const float4*)(x + lane * KS + i);
+        xl[i] = v.x;
+        xl[i + 1] = v.y;
+        xl[i + 2] = v.z;
+        xl[i + 3] = v.w;
+    }
+}
+
+// value of channel slot j (< CW) in lane j: one store instruction per wave publishes them.
+// The values are wave-uniform (reduced sums), so v_writelane moves each into its lane (a
+// select chain on the lane id would be turned into a scratch-indexed array).
+template <int CW>
+__device__ __forceinline__ float lane_select(const float (&v)[CW]) {
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+        const int u = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v[j]));
+        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(r) : "s"(u), "n"(j));
+    }
+    return __builtin_bit_cast(float, r);
+}
+
+}  // namespace
+
+template <typename WT, int KS>
+__global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipeParams p) {
+    constexpr int CWK = kPipeCwK, CWP = kPipeCwP;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int abort_flag;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wg = blockIdx.x;
+    const int C = p.C, nb = p.nb, nl = p.nl, Q = p.queue;
+    const int nE = 2 * nb + 1;
+    // per-role parameters selected with compile-time indices (a runtime index into the
+    // by-value kernel argument would copy it to scratch)
+    int role = -1, gi = 0, gn = 1, N = 0, Kpr = 0, Nout = 0, K0 = 0, d = 1, R = 0;
+    const void* Wr = nullptr;
+    const float* scr = nullptr;
+    const float* shr = nullptr;
+#pragma unroll
+    for (int l = 0; l < kStreamMaxLayers; ++l) {
+        if (l < nl && wg >= p.cu0[l] && wg < p.cu0[l + 1]) {
+            role = l;
+            gi = wg - p.cu0[l];
+            gn = p.cu0[l + 1] - p.cu0[l];
+            N = p.N[l];
+            Kpr = p.Kp[l];
+            Wr = p.W[l];
+            scr = p.scale[l];
+            shr = p.shift[l];
+        }
+        if (l == nl - 1) Nout = p.N[l];
+    }
+    if (role < 0) return;
+    K0 = p.Kp[0];
+    const int c_lo = (int)((int64_t)N * gi / gn), c_hi = (int)((int64_t)N * (gi + 1) / gn);
+    const bool is_expand = role == 0, is_shrink = role == nl - 1;
+    const bool is_k = !is_expand && !is_shrink && (role & 1);
+    const bool is_p = !is_expand && !is_shrink && !(role & 1);
+    const int b = is_k ? (role + 1) / 2 : role / 2;  // block of a k / p role
+#pragma unroll
+    for (int q = 1; q <= kStreamMaxBlocks; ++q)
+        if (q == b && is_k) {
+            d = p.dil[q];
+            R = p.ring[q];
+        }
+    if (tid == 0) abort_flag = 0;
+
+    // ---- LDS carve ----
+    float* xbuf = (float*)smem;               // 2 x C: swept input vector, by frame parity
+    float* rbuf = xbuf + 2 * C;               // 2 x kPipeMaxCh: residual slice, by parity
+    float* scl = rbuf + 2 * kPipeMaxCh;       // kPipeMaxCh scale, then kPipeMaxCh shift
+    float* xin = scl + 2 * kPipeMaxCh;        // expand: 2 x kPipeExpandK input vectors, by parity
+    float* hist = xin + 2 * kPipeExpandK;     // expand: frames t-1, t-2 (2 x cin0)
+    float* ring = hist + 2 * p.cin0;          // k-conv: [wave][R][CWK] partial sums
+
+    float* wring = ring + wid * R * CWK;
+
+    for (int c = c_lo + tid; c < c_hi; c += kThreads) {
+        scl[c - c_lo] = scr[c];
+        scl[kPipeMaxCh + c - c_lo] = shr[c];
+    }
+    float* gstate = p.state + (int64_t)wg * p.state_stride;
+    if (is_k)
+        for (int i = tid; i < kWaves * R * CWK; i += kThreads) ring[i] = gstate[i];
+    if (is_expand)
+        for (int i = tid; i < 2 * p.cin0; i += kThreads) hist[i] = gstate[i];
+    const int t0 = *p.frames_seen;
+    __syncthreads();
+
+    auto edge = [&](int e, int t) { return (const gu64*)p.gran + ((int64_t)(t & (Q - 1)) * nE + e) * C; };
+    auto out_edge = [&](int e, int t) { return (gu64*)p.gran + ((int64_t)(t & (Q - 1)) * nE + e) * C; };
+
+    if (is_expand) {
+        // ---- lane per channel: row c = c_lo + 64 wid + lane, Kp0 (<= 128) 16-bit weights ----
+        const int cin0 = p.cin0;
+        const int c = c_lo + wid * 64 + lane;
+        uint32_t w[kPipeExpandK / 2];
+#pragma unroll
+        for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = 0u;
+        if (c < c_hi) {
+            const uint32_t* src = (const uint32_t*)((const WT*)Wr + (int64_t)c * K0);
+#pragma unroll
+            for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = 2 * i < K0 ? src[i] : 0u;  // K0 <= kPipeExpandK
+        }
+        const float sc = c < c_hi ? scl[c - c_lo] : 0.f, sh = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
+        for (int s = 0; s < p.steps; ++s) {
+            const int t = t0 + s;
+            float* xv = xin + (s & 1) * kPipeExpandK;
+            const float* fr = p.frames + (int64_t)(t & (Q - 1)) * cin0;
+            for (int i = tid; i < cin0; i += kThreads) {
+                const float v = fr[i];
+                const float h1 = t == 0 ? v : hist[i];                          // frame t-1
+                const float h2 = t <= 1 ? (t == 0 ? v : h1) : hist[cin0 + i];   // frame t-2
+                xv[i] = h2;
+                xv[cin0 + i] = h1;
+                xv[2 * cin0 + i] = v;
+            }
+            for (int i = 3 * cin0 + tid; i < kPipeExpandK; i += kThreads) xv[i] = 0.f;
+            __syncthreads();
+            for (int i = tid; i < cin0; i += kThreads) {
+                hist[cin0 + i] = xv[cin0 + i];
+                hist[i] = xv[2 * cin0 + i];
+            }
+            if (c < c_hi) {
+                float a = 0.f;
+#pragma unroll
+                for (int i = 0; i < kPipeExpandK / 2; ++i) {
+                    a = __builtin_fmaf(lo16<WT>(w[i]), xv[2 * i], a);
+                    a = __builtin_fmaf(hi16<WT>(w[i]), xv[2 * i + 1], a);
+                }
+                float y = a * sc + sh;
+                y = y > 0.f ? y : 0.f;
+                publish(out_edge(0, t) + c, (unsigned)t + 1u, y);
+            }
+            // the next frame writes the other xin buffer; hist is rewritten only after the
+            // next barrier, which every wave passes after its reads of this frame
+        }
+        __syncthreads();
+        for (int i = tid; i < 2 * cin0; i += kThreads) gstate[i] = hist[i];
+    } else if (is_k) {
+        // ---- block b's k-conv: CWK rows per wave, NT = 3 taps, k-sliced ----
+        uint32_t w[3][CWK][KS / 2];
+        load_rows<WT, 3, CWK, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 3);
+        float sc[CWK], sh[CWK];
+        int nown = 0;
+#pragma unroll
+        for (int j = 0; j < CWK; ++j) {
+            const int c = c_lo + wid + kWaves * j;
+            sc[j] = c < c_hi ? scl[c - c_lo] : 0.f;
+            sh[j] = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
+            nown += c < c_hi;
+        }
+        for (int s = 0; s < p.steps; ++s) {
+            const int t = t0 + s;
+            float* xv = xbuf + (s & 1) * C;
+            if (!sweep(edge(role - 1, t), 0, C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid)) abort_flag = 1;
+            __syncthreads();
+            if (abort_flag) return;
+            float xl[KS];
+            load_x<KS>(xl, xv, lane);
+            float vn[CWK], out[CWK];
+            lane_dots<WT, 3, CWK, KS>(w, xl, 2, vn);
+#pragma unroll
+            for (int j = 0; j < CWK; ++j) vn[j] = wave_sum_uniform(vn[j]);
+            const int slot = t & (R - 1);
+            if (t == 0) {
+                // every tap reads x(0); outputs 1..2d start from the taps that still reach
+                // before the stream start
+                float v0[CWK], v1[CWK];
+                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0);
+                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1);
+#pragma unroll
+                for (int j = 0; j < CWK; ++j) {
+                    v0[j] = wave_sum_uniform(v0[j]);
+                    v1[j] = wave_sum_uniform(v1[j]);
+                    out[j] = (v0[j] + v1[j]) + vn[j];
+                    float y = out[j] * sc[j] + sh[j];
+                    out[j] = y > 0.f ? y : 0.f;
+                }
+                if (lane < nown)
+                    publish(out_edge(role, t) + c_lo + wid + kWaves * lane, (unsigned)t + 1u, lane_select<CWK>(out));
+                // ring: all slots zero, then outputs tt = 1..2d from the clamped taps
+                for (int i = lane; i < R * CWK; i += 64) wring[i] = 0.f;
+                if (lane < CWK) {
+                    for (int tt = 1; tt <= 2 * d; ++tt) {
+                        float a = 0.f;
+                        if (2 * d >= tt) a += lane_select<CWK>(v0);
+                        if (d >= tt) a += lane_select<CWK>(v1);
+                        wring[(tt & (R - 1)) * CWK + lane] = a;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < CWK; ++j) {
+                    float y = (wring[slot * CWK + j] + vn[j]) * sc[j] + sh[j];
+                    out[j] = y > 0.f ? y : 0.f;
+                }
+                if (lane < nown)
+                    publish(out_edge(role, t) + c_lo + wid + kWaves * lane, (unsigned)t + 1u, lane_select<CWK>(out));
+                // the older taps of x(t) feed outputs t + d (tap 1) and t + 2d (tap 0)
+                float v0[CWK], v1[CWK];
+                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1);
+                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0);
+#pragma unroll
+                for (int j = 0; j < CWK; ++j) {
+                    v1[j] = wave_sum_uniform(v1[j]);
+                    v0[j] = wave_sum_uniform(v0[j]);
+                }
+                if (lane < CWK) {
+                    wring[slot * CWK + lane] = 0.f;
+                    wring[((t + d) & (R - 1)) * CWK + lane] += lane_select<CWK>(v1);
+                    wring[((t + 2 * d) & (R - 1)) * CWK + lane] += lane_select<CWK>(v0);
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = tid; i < kWaves * R * CWK; i += kThreads) gstate[i] = ring[i];
+    } else {
+        // ---- block b's 1x1 conv (+ residual x_b(t)) or the shrink: CWP rows per wave ----
+        uint32_t w[1][CWP][KS / 2];
+        load_rows<WT, 1, CWP, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 1);
+        float sc[CWP], sh[CWP];
+        int nown = 0;
+#pragma unroll
+        for (int j = 0; j < CWP; ++j) {
+            const int c = c_lo + wid + kWaves * j;
+            sc[j] = c < c_hi ? scl[c - c_lo] : 0.f;
+            sh[j] = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
+            nown += c < c_hi;
+        }
+        for (int s = 0; s < p.steps; ++s) {
+            const int t = t0 + s;
+            float* xv = xbuf + (s & 1) * C;
+            float* rv = rbuf + (s & 1) * kPipeMaxCh;
+            bool ok = true;
+            if (is_p) ok = sweep(edge(role - 2, t) + c_lo, 0, c_hi - c_lo, (unsigned)t + 1u, rv, &abort_flag, p.err, tid);
+            if (ok) ok = sweep(edge(role - 1, t), 0, C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid);
+            if (!ok) abort_flag = 1;
+            __syncthreads();
+            if (abort_flag) return;
+            float xl[KS];
+            load_x<KS>(xl, xv, lane);
+            float v[CWP], out[CWP];
+            lane_dots<WT, 1, CWP, KS>(w, xl, 0, v);
+#pragma unroll
+            for (int j = 0; j < CWP; ++j) {
+                v[j] = wave_sum_uniform(v[j]);
+                const int c = c_lo + wid + kWaves * j;
+                float y = v[j] * sc[j] + sh[j];
+                if (is_p) {
+                    y = y > 0.f ? y : 0.f;
+                    y += c < c_hi ? rv[c - c_lo] : 0.f;
+                }
+                out[j] = y;
+            }
+            if (lane < nown) {
+                const float y = lane_select<CWP>(out);
+                const int c = c_lo + wid + kWaves * lane;
+                if (is_p)
+                    publish(out_edge(role, t) + c, (unsigned)t + 1u, y);
+                else
+                    p.poses[(int64_t)(t & (Q - 1)) * Nout + c] = y;
+            }
+        }
+    }
+    // ---- the last workgroup to finish advances the stream position (every workgroup read
+    // t0 above, before its arrival) ----
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        const unsigned prev = atomicAdd((unsigned*)p.arrivals, 1u);
+        int active = 0;
+#pragma unroll
+        for (int l = 0; l <= kStreamMaxLayers; ++l)
+            if (l == nl) active = p.cu0[l];
+        if (prev == (unsigned)active - 1u) {
+            *p.arrivals = 0u;
+            __hip_atomic_store(p.frames_seen, t0 + p.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+int stream_pipe_lds_bytes(int C, int cin0, int max_ring) {
+    return (2 * C + 2 * kPipeMaxCh + 2 * kPipeMaxCh + 2 * kPipeExpandK + 2 * cin0 + kWaves * max_ring * kPipeCwK) * 4;
+}
+
+hipError_t launch_stream_pipe(const StreamPipeParams& p, Act wtype, int lds_bytes, hipStream_t s) {
+    const dim3 grid(p.cu0[p.nl]);
+#define VP3D_PIPE(WT, KS) hipLaunchKernelGGL((stream_pipe_kernel<WT, KS>), grid, dim3(kThreads), lds_bytes, s, p)
+    const int KS = p.C / 64;
+    if (wtype == Act::F16 && KS == 16) VP3D_PIPE(_Float16, 16);
+    else if (wtype == Act::F16 && KS == 4) VP3D_PIPE(_Float16, 4);
+    else if (wtype == Act::BF16 && KS == 16) VP3D_PIPE(__bf16, 16);
+    else if (wtype == Act::BF16 && KS == 4) VP3D_PIPE(__bf16, 4);
+    else return hipErrorInvalidValue;
+#undef VP3D_PIPE
+    return hipGetLastError();
+}
+
+bool stream_pipe_channels_ok(int C) { return C == 1024 || C == 256; }
+
+}  // namespace vp3d
+
+namespace vp3d {
+
+hipError_t stream_pipe_prepare(Act wtype, int C, int lds_bytes) {
+    const void* f = nullptr;
+    if (wtype == Act::F16 && C == 1024) f = (const void*)stream_pipe_kernel<_Float16, 16>;
+    else if (wtype == Act::F16 && C == 256) f = (const void*)stream_pipe_kernel<_Float16, 4>;
+    else if (wtype == Act::BF16 && C == 1024) f = (const void*)stream_pipe_kernel<__bf16, 16>;
+    else if (wtype == Act::BF16 && C == 256) f = (const void*)stream_pipe_kernel<__bf16, 4>;
+    else return hipErrorInvalidValue;
+    return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+}
+
+}  // namespace vp3d

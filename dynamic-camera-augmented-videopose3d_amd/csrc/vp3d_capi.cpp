@@ -12,6 +12,7 @@
 //     TemporalModelOptimized1f._forward_blocks :188-198, one GEMM launch per conv
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -685,6 +686,13 @@ struct vp3d_stream {
     void* hand = nullptr;              // [16 B: timeout word][granules], zeroed before each launch
     size_t hand_bytes = 0;
     float* pstate = nullptr;           // per-workgroup partial rings + frame history
+    // layer-pipelined form (stream_pipe.hip): preferred over `persist` when it fits
+    bool pipe = false;
+    StreamPipeParams pipe_p{};
+    int pipe_lds = 0;
+    unsigned long long* pipe_gran = nullptr;  // [queue][2nb+1][C] granules, cleared at reset
+    size_t pipe_gran_bytes = 0;
+    float* pipe_state = nullptr;
 };
 
 namespace {
@@ -701,6 +709,12 @@ int pow2_at_least(int v) {
 // one GEMV launch per layer per step
 int stream_launch(vp3d_stream* st, hipStream_t s, int steps = 1) {
     const Act wt = st->dtype == VP3D_DTYPE_F32 ? Act::F32 : (st->dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16);
+    if (st->pipe) {
+        StreamPipeParams p = st->pipe_p;
+        p.steps = steps;
+        HIP_TRY(launch_stream_pipe(p, wt, st->pipe_lds, s));
+        return VP3D_OK;
+    }
     if (st->persist) {
         HIP_TRY(hipMemsetAsync(st->hand, 0, st->hand_bytes, s));
         StreamPersistParams p = st->pp;
@@ -790,6 +804,87 @@ bool stream_persist_setup(vp3d_stream* st, int dtype) {
     p.err = (unsigned*)st->hand;
     p.gran = (unsigned long long*)((char*)st->hand + 16);
     p.state = st->pstate;
+    return true;
+}
+
+// The layer-pipelined form's geometry (stream_pipe.hip): roles in layer order, each a
+// contiguous range of workgroups (one per CU).  Expand: ceil(C / 256) workgroups (one
+// channel per lane); shrink: ceil(N_out / 16); the rest split evenly over the blocks and,
+// inside a block, about 3 : 1 between the k-conv (3 taps) and the 1x1 conv -- the ratio
+// of their weights, so the per-frame work of the two groups is about equal.  False (the
+// LDS-resident persistent form is tried next) for shapes the kernel does not cover:
+// C other than 1024 / 256, k-convs other than 3 taps, an expand wider than 128 inputs.
+bool stream_pipe_setup(vp3d_stream* st, int dtype) {
+    const vp3d_handle* h = st->h;
+    if (dtype == VP3D_DTYPE_F32) return false;
+    const char* mode = getenv("VP3D_STREAM_MODE");
+    if (mode && strcmp(mode, "pipe")) return false;
+    const int nl = (int)h->layers.size(), nb = h->cfg.n_widths - 1, C = h->cfg.channels;
+    if (nl > kStreamMaxLayers || nb < 1 || nb > kStreamMaxBlocks || !stream_pipe_channels_ok(C)) return false;
+    const Layer& e = h->layers[0];
+    if (e.taps != 3 || e.dil != 1 || e.Kp > kPipeExpandK || e.cout != C) return false;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) return false;
+    const int nout = h->layers[nl - 1].cout;
+    const int n_e = (C + 255) / 256, n_s = (nout + 15) / 16;
+    const int per_block = (cus - n_e - n_s) / nb;
+    const int min_k = (C + 8 * kPipeCwK - 1) / (8 * kPipeCwK), min_p = (C + 8 * kPipeCwP - 1) / (8 * kPipeCwP);
+    int n_p = std::max(min_p, per_block / 4);
+    int n_k = per_block - n_p;
+    n_k = std::min(n_k, std::max(min_k, C / 8));   // small models: fewer, fuller workgroups
+    n_p = std::min(n_p, std::max(min_p, C / 16));
+    if (n_k < min_k || (nout + n_s - 1) / n_s > 8 * kPipeCwP) return false;
+    StreamPipeParams& p = st->pipe_p;
+    p = StreamPipeParams{};
+    p.nl = nl;
+    p.nb = nb;
+    p.C = C;
+    p.cin0 = e.cin;
+    int max_ring = 1;
+    for (int b = 1; b <= nb; ++b) {
+        const Layer& kc = h->layers[2 * b - 1];
+        const Layer& pc = h->layers[2 * b];
+        if (kc.taps != 3 || kc.Ktap != C || kc.K != 3 * C || kc.cout != C || pc.K != C || pc.cout != C) return false;
+        p.dil[b] = kc.dil;
+        p.ring[b] = pow2_at_least(2 * kc.dil + 1);
+        max_ring = std::max(max_ring, p.ring[b]);
+    }
+    if (h->layers[nl - 1].K != C) return false;
+    int g = 0;
+    for (int l = 0; l < nl; ++l) {
+        const Layer& L = h->layers[l];
+        p.W[l] = dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh;
+        p.scale[l] = L.scale;
+        p.shift[l] = L.shift;
+        p.Kp[l] = L.Kp;
+        p.N[l] = L.cout;
+        p.cu0[l] = g;
+        g += l == 0 ? n_e : (l == nl - 1 ? n_s : (l & 1 ? n_k : n_p));
+    }
+    p.cu0[nl] = g;
+    if (g > cus) return false;
+    const int lds = stream_pipe_lds_bytes(C, p.cin0, max_ring);
+    const Act wt = dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16;
+    if (lds > 160 * 1024 || stream_pipe_prepare(wt, C, lds) != hipSuccess) return false;
+    st->pipe_lds = lds;
+    p.state_stride = std::max(8 * max_ring * kPipeCwK, 2 * p.cin0);
+    st->pipe_gran_bytes = (size_t)kQueue * (2 * nb + 1) * C * 8;
+    if (hipMalloc(&st->pipe_gran, st->pipe_gran_bytes) != hipSuccess) return false;
+    if (hipMalloc(&st->pipe_state, (size_t)g * p.state_stride * 4) != hipSuccess) {
+        hipFree(st->pipe_gran);
+        st->pipe_gran = nullptr;
+        return false;
+    }
+    hipMemset(st->pipe_gran, 0, st->pipe_gran_bytes);
+    hipMemset(st->pipe_state, 0, (size_t)g * p.state_stride * 4);
+    p.frames = st->in_frame;
+    p.queue = kQueue;
+    p.poses = st->out_pose;
+    p.frames_seen = st->frames_seen;
+    p.arrivals = (unsigned*)(st->frames_seen + 2);
+    p.err = (unsigned*)(st->frames_seen + 3);
+    p.gran = st->pipe_gran;
+    p.state = st->pipe_state;
     return true;
 }
 
@@ -910,18 +1005,22 @@ int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
         q.done_counter = (unsigned*)(st->frames_seen + 1);
         st->steps.push_back(q);
     }
-    st->persist = stream_persist_setup(st, dtype);
+    st->pipe = stream_pipe_setup(st, dtype);
+    if (!st->pipe) st->persist = stream_persist_setup(st, dtype);
+    hipDeviceSynchronize();  // setup memsets (legacy stream) before any launch on another stream
     *out = st;
     return VP3D_OK;
 }
 
-int vp3d_stream_persistent(const vp3d_stream* st) { return st && st->persist ? 1 : 0; }
+int vp3d_stream_persistent(const vp3d_stream* st) { return st && (st->persist || st->pipe) ? 1 : 0; }
+
+int vp3d_stream_mode(const vp3d_stream* st) { return !st ? -1 : st->pipe ? 2 : st->persist ? 1 : 0; }
 
 int vp3d_stream_status(vp3d_stream* st) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
-    if (!st->persist) return VP3D_OK;
+    if (!st->persist && !st->pipe) return VP3D_OK;
     unsigned err = 0;
-    HIP_TRY(hipMemcpy(&err, st->hand, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&err, st->pipe ? (void*)(st->frames_seen + 3) : st->hand, 4, hipMemcpyDeviceToHost));
     if (err) return fail(VP3D_ERR_STATE, "persistent stream step timed out waiting for another CU");
     return VP3D_OK;
 }
@@ -929,6 +1028,8 @@ int vp3d_stream_status(vp3d_stream* st) {
 int vp3d_stream_reset(vp3d_stream* st, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     HIP_TRY(hipMemsetAsync(st->frames_seen, 0, 16, (hipStream_t)stream));
+    // pipelined form: granule tags restart at frame 1
+    if (st->pipe) HIP_TRY(hipMemsetAsync(st->pipe_gran, 0, st->pipe_gran_bytes, (hipStream_t)stream));
     st->host_t = 0;
     return VP3D_OK;
 }
@@ -978,7 +1079,7 @@ int vp3d_stream_graph_capture(vp3d_stream* st, void* stream, int steps) {
         hipGraphDestroy(st->graph);
         st->graph = nullptr;
     }
-    if (st->persist && steps > kQueue) return fail(VP3D_ERR_ARG, "a persistent graph runs at most queue_len steps");
+    if ((st->persist || st->pipe) && steps > kQueue) return fail(VP3D_ERR_ARG, "a persistent graph runs at most queue_len steps");
     HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int rc = stream_launch(st, s, steps);
     hipGraph_t g = nullptr;
@@ -1009,6 +1110,8 @@ int vp3d_stream_destroy(vp3d_stream* st) {
     hipFree(st->scratch);
     hipFree(st->hand);
     hipFree(st->pstate);
+    hipFree(st->pipe_gran);
+    hipFree(st->pipe_state);
     delete st;
     return VP3D_OK;
 }

@@ -20,7 +20,7 @@ BUILD_DIR = os.path.join(ROOT_PKG, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libvp3d.so")
 
 SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_8p.hip", "conv_gemm_q64.hip", "expand_gemm.hip", "preprocess.hip",
-           "metrics.hip", "stream_step.hip", "stream_persist.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp",
+           "metrics.hip", "stream_step.hip", "stream_persist.hip", "stream_pipe.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp",
            "vp3d_seq.cpp"]
 HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "gemm_common.h"), os.path.join(CSRC, "host.h"),
            os.path.join(INCLUDE, "vp3d.h")]

@@ -61,6 +61,12 @@ class CausalStream:
         in LDS); False for one GEMV launch per layer (fp32, or VP3D_STREAM_MODE=launches)."""
         return bool(self._lib.vp3d_stream_persistent(self._s))
 
+    @property
+    def mode(self) -> str:
+        """'pipe' (layer-pipelined persistent launch, stream_pipe.hip), 'persist' (every CU
+        runs every layer, weights in LDS, stream_persist.hip) or 'launches' (GEMV per layer)."""
+        return {2: "pipe", 1: "persist", 0: "launches"}[int(self._lib.vp3d_stream_mode(self._s))]
+
     def check(self) -> None:
         """Synchronise and raise if a persistent launch gave up waiting on another CU."""
         with torch.cuda.device(self.device):

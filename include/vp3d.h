@@ -173,6 +173,12 @@ int vp3d_stream_destroy(vp3d_stream* s);
  * resident in LDS, layer outputs handed between CUs in-launch), 0 for one GEMV launch
  * per layer (fp32 weights, or VP3D_STREAM_MODE=launches at vp3d_stream_create). */
 int vp3d_stream_persistent(const vp3d_stream* s);
+/* Form of the in-launch step: 2 = layer-pipelined (stream_pipe.hip: each CU runs one
+ * layer with its weights in VGPRs, frames of a batch pipelined through the layer groups;
+ * the default for 16-bit weights at 1024 / 256 channels with 3-tap blocks), 1 = every CU
+ * runs every layer with its weights in LDS (stream_persist.hip), 0 = one GEMV launch per
+ * layer.  VP3D_STREAM_MODE=pipe|persist|launches at vp3d_stream_create restricts it. */
+int vp3d_stream_mode(const vp3d_stream* s);
 /* Synchronises; VP3D_ERR_STATE if a persistent launch gave up waiting on another CU
  * (bounded spins: the grid did not fit the device at once), else VP3D_OK. */
 int vp3d_stream_status(vp3d_stream* s);

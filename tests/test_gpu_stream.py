@@ -45,10 +45,12 @@ def test_stream_matches_sequence(dtype, tol):
     np.testing.assert_allclose(first, out[0], atol=1e-7)
 
 
-@pytest.mark.parametrize("fw,channels", [((3, 3, 3, 3, 3), 1024), ((3, 5, 3), 256)])
-def test_stream_launches_form_matches_sequence(fw, channels, monkeypatch):
-    """VP3D_STREAM_MODE=launches keeps the per-layer GEMV form for 16-bit weights; both
-    forms agree with the whole-sequence reference (width-5 block: general taps)."""
+@pytest.mark.parametrize("fw,channels", [((3, 3, 3, 3, 3), 1024), ((3, 5, 3), 256), ((3, 3, 3), 256)])
+def test_stream_forms_match_sequence(fw, channels, monkeypatch):
+    """Every form of the fp16 step agrees with the whole-sequence reference:
+    VP3D_STREAM_MODE=launches (per-layer GEMVs), =persist (every CU runs every layer,
+    weights in LDS) and =pipe (one layer per CU, weights in VGPRs, frames pipelined
+    through the layer groups; a width-5 block is outside it and falls back to persist)."""
     m, sd = make_model(False, fw, causal=True, channels=channels)
     T = 120
     x = synth.normalized_windows(13, "stream_forms", 1, T)
@@ -56,31 +58,35 @@ def test_stream_launches_form_matches_sequence(fw, channels, monkeypatch):
     m.cuda()
     xs = torch.from_numpy(x[0]).cuda()
     outs = {}
-    for mode in ("launches", "persistent"):
-        if mode == "launches":
-            monkeypatch.setenv("VP3D_STREAM_MODE", "launches")
-        else:
-            monkeypatch.delenv("VP3D_STREAM_MODE", raising=False)
+    for mode in ("launches", "persist", "pipe"):
+        monkeypatch.setenv("VP3D_STREAM_MODE", mode)
         st = CausalStream(m.native_lifter(), "fp16")
-        assert st.persistent == (mode == "persistent")
+        want = "persist" if (mode == "pipe" and 5 in fw) else mode
+        assert st.mode == want, (mode, st.mode)
+        assert st.persistent == (want != "launches")
         outs[mode] = torch.stack([st.step(xs[t]).clone() for t in range(T)]).cpu().numpy()
         st.check()
         err = np.abs(outs[mode] - ref).max()
         print(f"stream fp16 {mode} fw={fw}: max|d|={err:.3e} m")
         assert err <= 3e-4
+    monkeypatch.delenv("VP3D_STREAM_MODE", raising=False)
+    st = CausalStream(m.native_lifter(), "fp16")
+    assert st.mode == ("persist" if 5 in fw else "pipe")
 
 
-def test_stream_graph_replay_matches_eager():
-    """Graphs of 1 and of 8 steps fed from the device frame queue reproduce the
-    eager per-step results bit for bit."""
-    fw = (3, 3, 3)
-    m, sd = make_model(False, fw, causal=True, channels=256)
-    T = 80
+@pytest.mark.parametrize("fw,channels,T,graphs", [((3, 3, 3), 256, 80, (1, 8)),
+                                                   ((3, 3, 3, 3, 3), 1024, 192, (64,))])
+def test_stream_graph_replay_matches_eager(fw, channels, T, graphs):
+    """Graphs of G steps fed from the device frame queue reproduce the eager per-step
+    results bit for bit -- in the pipelined form a graph of 64 steps is one launch with up
+    to 10 frames in flight through the layer groups, an eager step is a launch of one."""
+    m, sd = make_model(False, fw, causal=True, channels=channels)
     x = torch.from_numpy(synth.normalized_windows(12, "graph", 1, T)[0]).cuda().reshape(T, -1)
     m.cuda()
     eager = CausalStream(m.native_lifter(), "fp16")
     want = torch.stack([eager.step(x[t]).clone().reshape(-1) for t in range(T)])
-    for G in (1, 8):
+    eager.check()
+    for G in graphs:
         g = CausalStream(m.native_lifter(), "fp16")
         Q = g.queue_len
         assert T % G == 0 and Q % G == 0
