@@ -77,31 +77,38 @@ __device__ __forceinline__ void publish(gu64* g, unsigned tag, float v) {
     __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Poll granules [c_lo, c_hi) of one edge slot into x (LDS); every thread owns granules
-// c_lo + tid + j * kThreads (four in flight per pass).  False on timeout (sets the error
-// word and the workgroup's abort flag) or when another wave already aborted.
-__device__ bool sweep(const gu64* g, int c_lo, int c_hi, unsigned tag, float* x, volatile int* abort_flag,
-                      unsigned* err, int tid) {
-    const unsigned long long start = __builtin_amdgcn_s_memrealtime();
-    for (int i0 = c_lo + tid; i0 < c_hi; i0 += 4 * kThreads) {
-        unsigned pending = 0;
+// A sweep split in two so that the next frame's granule loads are in flight while the
+// current frame computes: pref_issue loads this thread's granules (tid, tid + kThreads of
+// an edge slice of n <= 2 * kThreads), pref_finish checks their tags, re-polls the ones
+// still missing (bounded, as sweep) and stores the values into x (LDS).
+struct Pref {
+    unsigned long long v[2];
+};
+
+__device__ __forceinline__ void pref_issue(Pref& r, const gu64* g, int n, int tid) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (i0 + j * kThreads < c_hi) pending |= 1u << j;
-        for (;;) {
-            unsigned long long v[4];
+    for (int j = 0; j < 2; ++j)
+        if (tid + j * kThreads < n) r.v[j] = __hip_atomic_load(g + tid + j * kThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* x, volatile int* abort_flag,
+                            unsigned* err, int tid) {
+    unsigned pending = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int i = i0 + j * kThreads < c_hi ? i0 + j * kThreads : c_hi - 1;
-                v[j] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int j = 0; j < 2; ++j)
+        if (tid + j * kThreads < n) pending |= 1u << j;
+    unsigned long long start = 0;
+    for (bool first = true;; first = false) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (((pending >> j) & 1u) && (unsigned)(r.v[j] >> 32) == tag) {
+                x[tid + j * kThreads] = __uint_as_float((unsigned)r.v[j]);
+                pending &= ~(1u << j);
             }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (((pending >> j) & 1u) && (unsigned)(v[j] >> 32) == tag) {
-                    x[i0 + j * kThreads - c_lo] = __uint_as_float((unsigned)v[j]);
-                    pending &= ~(1u << j);
-                }
-            if (!pending) break;
+        if (!pending) return true;
+        if (first) {
+            start = __builtin_amdgcn_s_memrealtime();
+        } else {
             if (*abort_flag) return false;
             if (__builtin_amdgcn_s_memrealtime() - start > kSpinTicks) {
                 *abort_flag = 1;
@@ -110,8 +117,11 @@ __device__ bool sweep(const gu64* g, int c_lo, int c_hi, unsigned tag, float* x,
             }
             __builtin_amdgcn_s_sleep(1);
         }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if ((pending >> j) & 1u)
+                r.v[j] = __hip_atomic_load(g + tid + j * kThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    return true;
 }
 
 // Lane-partial dot products of the wave's CW rows (NT taps each) with the lane's KS
@@ -308,12 +318,15 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             sh[j] = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
             nown += c < c_hi;
         }
+        Pref pf;
+        pref_issue(pf, edge(role - 1, t0), C, tid);
         for (int s = 0; s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
-            if (!sweep(edge(role - 1, t), 0, C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid)) abort_flag = 1;
+            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid)) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
+            if (s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
             float xl[KS];
             load_x<KS>(xl, xv, lane);
             float vn[CWK], out[CWK];
@@ -386,16 +399,23 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             sh[j] = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
             nown += c < c_hi;
         }
+        const int nres = is_p ? c_hi - c_lo : 0;
+        Pref pf, pr;
+        pref_issue(pr, edge(role - 2, t0) + c_lo, nres, tid);
+        pref_issue(pf, edge(role - 1, t0), C, tid);
         for (int s = 0; s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
             float* rv = rbuf + (s & 1) * kPipeMaxCh;
-            bool ok = true;
-            if (is_p) ok = sweep(edge(role - 2, t) + c_lo, 0, c_hi - c_lo, (unsigned)t + 1u, rv, &abort_flag, p.err, tid);
-            if (ok) ok = sweep(edge(role - 1, t), 0, C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid);
+            bool ok = pref_finish(pr, edge(role - 2, t) + c_lo, nres, (unsigned)t + 1u, rv, &abort_flag, p.err, tid);
+            if (ok) ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid);
             if (!ok) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
+            if (s + 1 < p.steps) {  // the next frame's loads are in flight during this one
+                pref_issue(pr, edge(role - 2, t + 1) + c_lo, nres, tid);
+                pref_issue(pf, edge(role - 1, t + 1), C, tid);
+            }
             float xl[KS];
             load_x<KS>(xl, xv, lane);
             float v[CWP], out[CWP];
