@@ -32,6 +32,7 @@
 // barrier lgkmcnt(0) [16 MFMAs at s_setprio 1] barrier; wave group 1 runs one barrier
 // behind group 0, so the two waves of a SIMD alternate memory and MFMA segments.
 #include <cstdlib>
+#include <cstring>
 
 #include "gemm_common.h"
 
@@ -60,9 +61,24 @@ __device__ __forceinline__ void qvm() {
 }
 
 // EPI (measurement builds only, tools/ubench/gemm_check with VP3D_ABL): 0 = the epilogue,
-// 1 = stores issued but dropped by the range check (no output traffic), 2 = no epilogue
+// 1 = stores issued but dropped by the range check (no output traffic), 2 = no epilogue,
+// 3 = the epilogue without the residual loads
+#ifdef VP3D_ABLATION
+// measurement builds only: first-round workgroups of CU group g = (bid >> 3) % groups sleep
+// g * iters x 127 x 64 cycles before starting, so their tiles' epilogues (output + residual
+// traffic) fall at different times across the chip (VP3D_STAGGER=iters[,groups])
+__device__ int g_stagger_iters;
+__device__ int g_stagger_groups;
+#endif
+
 template <typename CT, int EPI = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
+#ifdef VP3D_ABLATION
+    if (g_stagger_iters > 0 && blockIdx.x < 256) {
+        const int n = ((blockIdx.x >> 3) % g_stagger_groups) * g_stagger_iters;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     __shared__ __attribute__((aligned(16))) char smem[2 * QBUF + 2 * QMAXN * 4];
     float* const s_scale = (float*)(smem + 2 * QBUF);
     float* const s_shift = s_scale + QMAXN;
@@ -246,7 +262,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
     // the residual (1x1 convs) is loaded inside the epilogue, one row block ahead of its
     // use (issuing all 16 loads of the block when the K loop ends measured the same:
     // block-1 1x1 + residual 0.674 vs 0.667 ms -- per-CU bandwidth, not latency)
-    if (p.R)
+    if (p.R && EPI != 3)
         epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc,
                                         nullptr, m0);
     else
@@ -273,11 +289,20 @@ hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_
 #ifdef VP3D_ABLATION
     static const int abl = [] {
         const char* e = getenv("VP3D_ABL");
+        const char* st = getenv("VP3D_STAGGER");
+        if (st) {
+            int it = atoi(st), gr = 2;
+            if (const char* c = strchr(st, ',')) gr = atoi(c + 1);
+            if (gr < 1) gr = 1;
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stagger_iters), &it, sizeof(int));
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stagger_groups), &gr, sizeof(int));
+        }
         return e ? atoi(e) : 0;
     }();
-    if (compute == Act::BF16 && (abl == 1 || abl == 2)) {
+    if (compute == Act::BF16 && (abl >= 1 && abl <= 3)) {
         if (abl == 1) hipLaunchKernelGGL((conv_gemm_q64<__bf16, 1>), grid, dim3(512), 0, stream, p);
-        else hipLaunchKernelGGL((conv_gemm_q64<__bf16, 2>), grid, dim3(512), 0, stream, p);
+        else if (abl == 2) hipLaunchKernelGGL((conv_gemm_q64<__bf16, 2>), grid, dim3(512), 0, stream, p);
+        else hipLaunchKernelGGL((conv_gemm_q64<__bf16, 3>), grid, dim3(512), 0, stream, p);
         return hipGetLastError();
     }
 #endif
