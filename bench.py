@@ -201,8 +201,16 @@ def stream_main(args, world, rank, dev):
                    "frames_per_step": 1, "steps_per_graph": G, "mode": mode, "parallelism": f"replicas{world}"},
         "roofline": {"bound": "hbm", "kernel": {"pipe": "stream_pipe_kernel", "persist": "stream_persist_kernel",
                                                 "launches": "stream step (10 stream_gemv launches)"}[mode],
-                     "note": "achieved = the step's weight bytes / step time (the unit of work of a "
-                             "weight-streaming step; in the persistent form the weights stay in LDS)",
+                     "note": "achieved = the step's weight bytes / step time: the unit of work of a "
+                             "weight-streaming step, whose 8 TB/s roofline is "
+                             f"{step_bytes / 8e12 * 1e6:.2f} us/step. "
+                             + ({"pipe": "Here the weights stay resident in VGPRs (persist: LDS) for the whole "
+                                         "launch, so frac > 1 is possible: the step period is set by the "
+                                         "inter-CU hand-off latency of the layer pipeline, not by HBM.",
+                                 "persist": "Here the weights stay resident in LDS for the whole launch, so "
+                                            "frac > 1 is possible: the step is bound by the hand-off latency "
+                                            "between layers, not by HBM.",
+                                 "launches": "The weights are re-read every step."}[mode]),
                      "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
                      "frac": round(achieved / 8000.0, 4), "traffic": None,
                      "bytes_per_step": step_bytes, "avg_step_us": round(step_s * 1e6, 3)},
