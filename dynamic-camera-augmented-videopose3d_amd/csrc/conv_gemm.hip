@@ -324,6 +324,7 @@ hipError_t launch_f32(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t
 //   from rows d apart; sequence mode, 65,536 frames: 0.39-0.40 vs 0.42 ms).
 //   VP3D_GEMM=q64 / 8p -> that kernel wherever eligible (dilated layers included),
 //   VP3D_GEMM=big -> the LDS-ring kernel everywhere; the override test runs all three.
+//   VP3D_GEMM=h16 -> the 128x128 kernel everywhere (measurement).
 //   The round-1 A/B schedules (persistent, dynamic-queue, older ping-pong, transposed
 //   persistent) were 3-10 % slower and live outside the library, in tools/ubench/retired/.
 //   Read at every launch (a getenv per layer is noise next to the kernel), so a test can
@@ -333,6 +334,7 @@ int gemm_8p_mode() {
     if (!e) return 1;
     if (strcmp(e, "8p") == 0) return 2;
     if (strcmp(e, "q64") == 0) return 3;
+    if (strcmp(e, "h16") == 0) return 4;  // the 128x128 kernel everywhere (measurement)
     return strcmp(e, "big") == 0 ? 0 : 1;
 }
 bool gemm_8p_env(const ConvGemmParams& p) {
@@ -452,7 +454,8 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_8p_eligible(p, a_type, out_type, compute))
         return launch_conv_gemm_8p(p, compute, stream);
-    if (conv_gemm_big_eligible(p, a_type, out_type, compute)) return launch_conv_gemm_big(p, out_type, compute, stream);
+    if (gm != 4 && conv_gemm_big_eligible(p, a_type, out_type, compute))
+        return launch_conv_gemm_big(p, out_type, compute, stream);
     const int aes = a_type == Act::F32 ? 4 : 2;
     int amode = A_SCALAR;
     if ((p.Ktap % kH16Bk == 0) && (p.lda % 8 == 0) && aligned(p.A, 16))
