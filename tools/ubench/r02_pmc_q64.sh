@@ -3,7 +3,7 @@
 # breakdown, MFMA busy, LDS waits / bank conflicts, TA busy, L2 hit rate.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r02g; mkdir -p $OUT
+OUT=gpurun_out/${PMC_TAG:-r02g}; mkdir -p $OUT
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
 P2="TA_BUSY_avr TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
 for k in q64 8p; do

@@ -1,13 +1,19 @@
 """Calibration (tool, not product): hipBLASLt bf16 GEMM rate (torch.matmul) on the
-lifter's layer shapes at B = 8192 windows, for comparison with the conv-GEMM kernels."""
+lifter's layer shapes at B = 8192 windows (TORCH_GEMM_B=65536 for the config-4 batch), for
+comparison with the conv-GEMM kernels.  Under rocprofv3 --kernel-trace the kernel names show
+hipBLASLt's tile configuration."""
+import os
+
 import torch
 
+B = int(os.environ.get("TORCH_GEMM_B", "8192"))
+
 shapes = {  # name: (M, N, K)
-    "expand": (8192 * 81, 1024, 128),
-    "block1_k3": (8192 * 27, 1024, 3072),
-    "block1_1x1": (8192 * 27, 1024, 1024),
-    "block2_k3": (8192 * 9, 1024, 3072),
-    "block3_k3": (8192 * 3, 1024, 3072),
+    "expand": (B * 81, 1024, 128),
+    "block1_k3": (B * 27, 1024, 3072),
+    "block1_1x1": (B * 27, 1024, 1024),
+    "block2_k3": (B * 9, 1024, 3072),
+    "block3_k3": (B * 3, 1024, 3072),
 }
 for name, (M, N, K) in shapes.items():
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
