@@ -23,8 +23,8 @@
 //   Q0 (h0, g0): read A_h0 (8 ds_read_b128) + W_g0 (4)   issue A_h0 of tile t+1
 //   Q1 (h0, g1): read W_g1 (4)                            issue W_g0 of t+1
 //   Q2 (h1, g1): read A_h1 (8)                            issue W_g1 of t+1
-//   Q3 (h1, g0): read W_g0 (4) again                      issue A_h1 of t+1
-// (W_g0 is re-read in Q3 rather than kept in 16 more VGPRs.)  A region (A_h* / W_g*) is re-staged >= 2 phases after its last
+//   Q3 (h1, g0): (W_g0 still in registers)               issue A_h1 of t+1
+// (W_g0 is kept in 16 more VGPRs rather than re-read in Q3: 0.6-0.9 % faster.)  A region (A_h* / W_g*) is re-staged >= 2 phases after its last
 // read, its reads retired before the barrier that ends their phase (WAR), and read 3
 // phases after its DMA was issued; each wave waits (vmcnt(4), never 0 in steady state) in the
 // memory segment of the phase BEFORE the one that reads the region, which precedes that
@@ -71,7 +71,7 @@ __device__ int g_stagger_iters;
 __device__ int g_stagger_groups;
 #endif
 
-template <typename CT, int EPI = 0>
+template <typename CT, int EPI = 0, int PH3 = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
 #ifdef VP3D_ABLATION
     if (g_stagger_iters > 0 && blockIdx.x < 256) {
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     u32x4 af[4][2];  // A fragments of the current row half: [row block][kh]
-    u32x4 bf[2][2];  // W fragments of the current channel half: [block jj][kh]
+    u32x4 bf[2][2][2];  // W fragments of both channel halves: [g][block jj][kh]
 
     auto read_a = [&](const char* buf, int h) {
 #pragma unroll
@@ -173,12 +173,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
             af[i][1] = *(const u32x4*)(r + fo1);
         }
     };
+    // both channel halves' W fragments stay in registers for the whole K-tile, so Q3 reads
+    // nothing (24 instead of 28 KiB of LDS reads per wave per K-tile; re-reading W_g0 in Q3
+    // instead of holding 16 more VGPRs measured 0.6-0.9 % slower)
     auto read_w = [&](const char* buf, int g) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
             const char* r = buf + w_base + (g * 32 + jj * 16) * 128;
-            bf[jj][0] = *(const u32x4*)(r + fo0);
-            bf[jj][1] = *(const u32x4*)(r + fo1);
+            bf[g][jj][0] = *(const u32x4*)(r + fo0);
+            bf[g][jj][1] = *(const u32x4*)(r + fo1);
         }
     };
     auto mma = [&](int h, int g) {
@@ -189,7 +192,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int jj = 0; jj < 2; ++jj)
-                    acc[4 * h + i][2 * g + jj] = mfma16<CT>(bf[jj][kh], af[i][kh], acc[4 * h + i][2 * g + jj]);
+                    acc[4 * h + i][2 * g + jj] =
+                        mfma16<CT>(bf[g][jj][kh], af[i][kh], acc[4 * h + i][2 * g + jj]);
         __builtin_amdgcn_s_setprio(0);
     };
     auto compute_seg = [&](int h, int g) {
@@ -232,12 +236,27 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
             qvm<0>();
         }
         compute_seg(0, 1);
+        if (PH3) {
+            // ---- Q2+Q3 as one phase of 32 MFMAs (A/B: 6 barriers per K-tile instead of 8):
+            // A_h1; stage W_g1(t+1), A_h1(t+1); wait A_h0(t+1), W_g0(t+1) ----
+            read_a(buf, 1);
+            if (more) {
+                issue(t + 1, 2);
+                issue(t + 1, 3);
+                qvm<4>();  // younger: W_g1(t+1), A_h1(t+1)
+            }
+            qbarrier();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            mma(1, 1);
+            mma(1, 0);
+            qbarrier();
+            continue;
+        }
         // ---- Q2: A_h1; stage W_g1(t+1) ----
         read_a(buf, 1);
         if (more) issue(t + 1, 2);
         compute_seg(1, 1);
-        // ---- Q3: W_g0 again; stage A_h1(t+1); wait A_h0(t+1), W_g0(t+1) ----
-        read_w(buf, 0);
+        // ---- Q3: W_g0 (kept in registers since Q0); stage A_h1(t+1); wait A_h0(t+1), W_g0(t+1) ----
         if (more) {
             issue(t + 1, 3);
             qvm<4>();  // younger: W_g1(t+1), A_h1(t+1)
@@ -299,6 +318,10 @@ hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_
         }
         return e ? atoi(e) : 0;
     }();
+    if (compute == Act::BF16 && abl == 4) {
+        hipLaunchKernelGGL((conv_gemm_q64<__bf16, 0, 1>), grid, dim3(512), 0, stream, p);
+        return hipGetLastError();
+    }
     if (compute == Act::BF16 && (abl >= 1 && abl <= 3)) {
         if (abl == 1) hipLaunchKernelGGL((conv_gemm_q64<__bf16, 1>), grid, dim3(512), 0, stream, p);
         else if (abl == 2) hipLaunchKernelGGL((conv_gemm_q64<__bf16, 2>), grid, dim3(512), 0, stream, p);
