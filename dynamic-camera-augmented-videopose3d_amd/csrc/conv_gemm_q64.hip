@@ -19,17 +19,18 @@
 // stored at chunk c ^ ((r >> 1) & 7) (conflict-free ds_read_b128 for the fragment reads;
 // the swizzle is applied to each lane's SOURCE address, the DMA writes lane-linearly).
 //
-// K-tile t = 4 phases (quadrants of the wave's 128 x 64 tile: rows h, channels g):
-//   Q0 (h0, g0): read A_h0 (8 ds_read_b128) + W_g0 (4)   issue A_h0 of tile t+1
-//   Q1 (h0, g1): read W_g1 (4)                            issue W_g0 of t+1
-//   Q2 (h1, g1): read A_h1 (8)                            issue W_g1 of t+1
-//   Q3 (h1, g0): (W_g0 still in registers)               issue A_h1 of t+1
-// (W_g0 is kept in 16 more VGPRs rather than re-read in Q3: 0.6-0.9 % faster.)  A region (A_h* / W_g*) is re-staged >= 2 phases after its last
-// read, its reads retired before the barrier that ends their phase (WAR), and read 3
-// phases after its DMA was issued; each wave waits (vmcnt(4), never 0 in steady state) in the
-// memory segment of the phase BEFORE the one that reads the region, which precedes that
-// read by a barrier for both wave groups (RAW).  Each phase: [reads + 2 DMA pieces + wait]
-// barrier lgkmcnt(0) [16 MFMAs at s_setprio 1] barrier; wave group 1 runs one barrier
+// K-tile t = 3 phases over the quadrants of the wave's 128 x 64 tile (rows h, channels g):
+//   Q0  (h0, g0):            read A_h0 (8 ds_read_b128) + W_g0 (4)   issue A_h0 of tile t+1
+//   Q1  (h0, g1):            read W_g1 (4)                            issue W_g0 of t+1
+//   Q23 (h1, g1) + (h1, g0): read A_h1 (8)                            issue W_g1, A_h1 of t+1
+// W_g0 stays in 16 more VGPRs from Q0 to Q23 (re-reading it measured 0.6-0.9 % slower), and
+// Q2 / Q3 share one 32-MFMA phase (two barriers fewer per K-tile: block-1 k3 -3.3 %).  A
+// region (A_h* / W_g*) is re-staged >= 2 phases after its last read, its reads retired
+// before the barrier that ends their phase (WAR), and read >= 2 phases after its DMA was
+// issued; each wave waits (vmcnt(4), never 0 in steady state) in the memory segment of the
+// phase BEFORE the one that reads the region, which precedes that read by a barrier for both
+// wave groups (RAW).  Each phase: [reads + DMA pieces + wait] barrier lgkmcnt(0) [16 or 32
+// MFMAs at s_setprio 1] barrier; wave group 1 runs one barrier
 // behind group 0, so the two waves of a SIMD alternate memory and MFMA segments.
 #include <cstdlib>
 #include <cstring>
@@ -71,7 +72,7 @@ __device__ int g_stagger_iters;
 __device__ int g_stagger_groups;
 #endif
 
-template <typename CT, int EPI = 0, int PH3 = 0>
+template <typename CT, int EPI = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
 #ifdef VP3D_ABLATION
     if (g_stagger_iters > 0 && blockIdx.x < 256) {
@@ -173,9 +174,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
             af[i][1] = *(const u32x4*)(r + fo1);
         }
     };
-    // both channel halves' W fragments stay in registers for the whole K-tile, so Q3 reads
-    // nothing (24 instead of 28 KiB of LDS reads per wave per K-tile; re-reading W_g0 in Q3
-    // instead of holding 16 more VGPRs measured 0.6-0.9 % slower)
+    // both channel halves' W fragments stay in registers for the whole K-tile, so the h1
+    // quadrants read only A_h1 (24 instead of 28 KiB of LDS reads per wave per K-tile;
+    // re-reading W_g0 instead of holding 16 more VGPRs measured 0.6-0.9 % slower)
     auto read_w = [&](const char* buf, int g) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
@@ -236,32 +237,19 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
             qvm<0>();
         }
         compute_seg(0, 1);
-        if (PH3) {
-            // ---- Q2+Q3 as one phase of 32 MFMAs (A/B: 6 barriers per K-tile instead of 8):
-            // A_h1; stage W_g1(t+1), A_h1(t+1); wait A_h0(t+1), W_g0(t+1) ----
-            read_a(buf, 1);
-            if (more) {
-                issue(t + 1, 2);
-                issue(t + 1, 3);
-                qvm<4>();  // younger: W_g1(t+1), A_h1(t+1)
-            }
-            qbarrier();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            mma(1, 1);
-            mma(1, 0);
-            qbarrier();
-            continue;
-        }
-        // ---- Q2: A_h1; stage W_g1(t+1) ----
+        // ---- Q2 + Q3 as one phase of 32 MFMAs (h1 x both channel halves; W_g0 still in
+        // registers since Q0): A_h1; stage W_g1(t+1), A_h1(t+1); wait A_h0(t+1), W_g0(t+1) ----
         read_a(buf, 1);
-        if (more) issue(t + 1, 2);
-        compute_seg(1, 1);
-        // ---- Q3: W_g0 (kept in registers since Q0); stage A_h1(t+1); wait A_h0(t+1), W_g0(t+1) ----
         if (more) {
+            issue(t + 1, 2);
             issue(t + 1, 3);
             qvm<4>();  // younger: W_g1(t+1), A_h1(t+1)
         }
-        compute_seg(1, 0);
+        qbarrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mma(1, 1);
+        mma(1, 0);
+        qbarrier();
     }
     if (wr == 0) qbarrier();  // match group 1's extra barrier
 
@@ -318,10 +306,6 @@ hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_
         }
         return e ? atoi(e) : 0;
     }();
-    if (compute == Act::BF16 && abl == 4) {
-        hipLaunchKernelGGL((conv_gemm_q64<__bf16, 0, 1>), grid, dim3(512), 0, stream, p);
-        return hipGetLastError();
-    }
     if (compute == Act::BF16 && (abl >= 1 && abl <= 3)) {
         if (abl == 1) hipLaunchKernelGGL((conv_gemm_q64<__bf16, 1>), grid, dim3(512), 0, stream, p);
         else if (abl == 2) hipLaunchKernelGGL((conv_gemm_q64<__bf16, 2>), grid, dim3(512), 0, stream, p);
