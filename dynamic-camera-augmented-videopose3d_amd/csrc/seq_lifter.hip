@@ -405,27 +405,51 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 
 // Stacked LSTM over W steps for a tile of NW windows.  Thread (u, half): hidden unit u
 // (0..H-1) of windows [half*NWH, half*NWH + NWH); it owns that unit's four gates and
-// cell state.  Weights are read transposed ([k][4H], coalesced across units); the
-// previous hidden states of the tile live in LDS.
-constexpr int LSTM_NW = 16;
+// cell state.  Weights are read transposed ([k][4H], coalesced across units) from L2 every
+// step, once per tile: the tile width NW sets how often the whole recurrence re-reads them
+// (NW = 32 for <= 2 layers, the run.py configuration: half the weight traffic of NW = 16,
+// the hidden states of both layers in 64 KiB of LDS).  The previous hidden states of the
+// tile live in LDS and are read 4 units at a time (ds_read_b128, broadcast across the
+// wave); every gate sum still accumulates k in ascending order.
 constexpr int LSTM_MAXL = 4;
 
-template <int H>
+template <int H, int NW, int MAXL>
 __global__ __launch_bounds__(2 * H) void lstm_kernel(LstmParams p) {
-    constexpr int NWH = LSTM_NW / 2;
-    __shared__ float hs[LSTM_MAXL][2][LSTM_NW][H];  // [layer][buffer][window][unit]
+    constexpr int NWH = NW / 2;
+    __shared__ __attribute__((aligned(16))) float hs[MAXL][2][NW][H];  // [layer][buffer][window][unit]
     const int u = threadIdx.x % H;
     const int half = threadIdx.x / H;
-    const int w0 = blockIdx.x * LSTM_NW;
-    for (int e = threadIdx.x; e < LSTM_MAXL * 2 * LSTM_NW * H; e += blockDim.x) (&hs[0][0][0][0])[e] = 0.f;
-    float c[LSTM_MAXL][NWH];
+    const int w0 = blockIdx.x * NW;
+    for (int e = threadIdx.x; e < MAXL * 2 * NW * H; e += blockDim.x) (&hs[0][0][0][0])[e] = 0.f;
+    float c[MAXL][NWH];
 #pragma unroll
-    for (int l = 0; l < LSTM_MAXL; ++l)
+    for (int l = 0; l < MAXL; ++l)
 #pragma unroll
         for (int i = 0; i < NWH; ++i) c[l][i] = 0.f;
     __syncthreads();
     const int G = 4 * H;
     int cur = 0;
+    // acc[q][i] += sum_k h[i][k] * WT[k][q*H + u], k ascending
+    auto gemv = [&](float (&acc)[4][NWH], const float* WT, const float* h) {
+        for (int k = 0; k < H; k += 4) {
+            float wv[4][4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) wv[kk][q] = WT[(k + kk) * G + q * H + u];
+#pragma unroll
+            for (int i = 0; i < NWH; ++i) {
+                const float4 hv = *(const float4*)&h[i * H + k];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    acc[q][i] = fmaf(hv.x, wv[0][q], acc[q][i]);
+                    acc[q][i] = fmaf(hv.y, wv[1][q], acc[q][i]);
+                    acc[q][i] = fmaf(hv.z, wv[2][q], acc[q][i]);
+                    acc[q][i] = fmaf(hv.w, wv[3][q], acc[q][i]);
+                }
+            }
+        }
+    };
     for (int t = 0; t < p.W; ++t) {
         for (int l = 0; l < p.L; ++l) {
             float acc[4][NWH];
@@ -442,47 +466,19 @@ __global__ __launch_bounds__(2 * H) void lstm_kernel(LstmParams p) {
                     for (int q = 0; q < 4; ++q) acc[q][i] = p.bias[l][q * H + u];
                 }
             }
-            if (l > 0) {
-                const float* WT = p.wih_t[l];  // [H][4H]
-                const float* hin = &hs[l - 1][cur ^ 1][half * NWH][0];
-                for (int k = 0; k < H; ++k) {
-                    float wv[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) wv[q] = WT[k * G + q * H + u];
-#pragma unroll
-                    for (int i = 0; i < NWH; ++i) {
-                        const float hv = hin[i * H + k];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) acc[q][i] = fmaf(hv, wv[q], acc[q][i]);
-                    }
-                }
-            }
-            {
-                const float* WT = p.whh_t[l];
-                const float* hprev = &hs[l][cur][half * NWH][0];
-                for (int k = 0; k < H; ++k) {
-                    float wv[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) wv[q] = WT[k * G + q * H + u];
-#pragma unroll
-                    for (int i = 0; i < NWH; ++i) {
-                        const float hv = hprev[i * H + k];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) acc[q][i] = fmaf(hv, wv[q], acc[q][i]);
-                    }
-                }
-            }
+            if (l > 0) gemv(acc, p.wih_t[l], &hs[l - 1][cur ^ 1][half * NWH][0]);
+            gemv(acc, p.whh_t[l], &hs[l][cur][half * NWH][0]);
 #pragma unroll
             for (int i = 0; i < NWH; ++i) {
                 const float ig = sigm(acc[0][i]), fg = sigm(acc[1][i]);
                 const float gg = tanhf(acc[2][i]), og = sigm(acc[3][i]);
                 float cc = c[0][0];
 #pragma unroll
-                for (int ll = 0; ll < LSTM_MAXL; ++ll)
+                for (int ll = 0; ll < MAXL; ++ll)
                     if (ll == l) cc = c[ll][i];
                 cc = fg * cc + ig * gg;
 #pragma unroll
-                for (int ll = 0; ll < LSTM_MAXL; ++ll)
+                for (int ll = 0; ll < MAXL; ++ll)
                     if (ll == l) c[ll][i] = cc;
                 hs[l][cur ^ 1][half * NWH + i][u] = og * tanhf(cc);
             }
@@ -581,10 +577,14 @@ hipError_t launch_attention(const float* QKV, int n_win, int W, int d, int heads
 
 hipError_t launch_lstm(const LstmParams& p, hipStream_t s) {
     if (p.L < 1 || p.L > LSTM_MAXL) return hipErrorInvalidValue;
-    const dim3 grid((p.n_win + LSTM_NW - 1) / LSTM_NW);
+    if (p.H == 128 && p.L <= 2) {
+        hipLaunchKernelGGL((lstm_kernel<128, 32, 2>), dim3((p.n_win + 31) / 32), dim3(256), 0, s, p);
+        return hipGetLastError();
+    }
+    const dim3 grid((p.n_win + 15) / 16);
     switch (p.H) {
-        case 64: hipLaunchKernelGGL(lstm_kernel<64>, grid, dim3(128), 0, s, p); break;
-        case 128: hipLaunchKernelGGL(lstm_kernel<128>, grid, dim3(256), 0, s, p); break;
+        case 64: hipLaunchKernelGGL((lstm_kernel<64, 16, LSTM_MAXL>), grid, dim3(128), 0, s, p); break;
+        case 128: hipLaunchKernelGGL((lstm_kernel<128, 16, LSTM_MAXL>), grid, dim3(256), 0, s, p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
