@@ -95,11 +95,13 @@ def test_opt1f_outputs_past_2gb_bf16():
     assert np.abs(y - ref[None]).max() <= H16_TOL["bf16"][0]
 
 
-@pytest.mark.parametrize("gemm,opt1f", [("big", True), ("8p", True), ("8p", False), ("q64", False)])
+@pytest.mark.parametrize("gemm,opt1f", [("big", True), ("8p", True), ("8p", False), ("q64", False),
+                                        ("h16", True), ("h16", False)])
 def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
     """Every 256x256 kernel on the shapes the default dispatch gives another one:
     VP3D_GEMM=big / 8p put the strided block convs (B = 2050) on the LDS-ring / ping-pong
-    kernel, VP3D_GEMM=8p / q64 the dilated convs of a long sequence on those kernels."""
+    kernel, VP3D_GEMM=8p / q64 the dilated convs of a long sequence on those kernels;
+    VP3D_GEMM=h16 (measurement override) every large layer on the 128x128 kernel."""
     monkeypatch.setenv("VP3D_GEMM", gemm)
     if opt1f:
         y, ref, gt = _run(True, 2050, 243, dtype="bf16")
