@@ -1,0 +1,64 @@
+"""The bench JSON contract, checked on the committed MI355X bench lines (CPU only).
+
+bench.py prints one JSON line per run; the driver and the judge read `metric`, `value`,
+`unit`, the timing fields, `roofline` (dominant kernel against its peak, with the PMC
+traffic) and `cpu_baseline` (the oracle on the host cores).  These tests pin that shape on
+the lines profiles/ holds for the headline run (config 4, N = 1), so a bench change that
+drops or renames a field fails here before it reaches a GPU box.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROFILES = os.path.join(REPO, "profiles")
+HEADLINE = ["r02h_bench_bf16.json", "r02l_bench_default.json"]
+
+
+def _line(name):
+    with open(os.path.join(PROFILES, name)) as f:
+        return json.loads(f.read().strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("name", HEADLINE)
+def test_headline_line_fields(name):
+    d = _line(name)
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert d["metric"] == base["metric"]
+    for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["vs_baseline"] is None
+    assert d["scaling"] == "strong" and d["config"]["global_batch"] == 65536
+    assert "workload" in d["config"] and "model" not in d["config"]
+    # value = global batch x steps / wall time; ms_per_step is the same clock
+    assert d["value"] == pytest.approx(65536 / (d["ms_per_step"] * 1e-3), rel=1e-3)
+
+
+@pytest.mark.parametrize("name", HEADLINE)
+def test_roofline_and_cpu_baseline(name):
+    d = _line(name)
+    r = d["roofline"]
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] in ("GB/s", "TFLOP/s")
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    assert r["peak"] == 2500.0  # bf16 dense MFMA peak (MI355X_MICROARCH.md)
+    # achieved = algorithmic FLOP of the launch / its mean duration
+    assert r["achieved"] == pytest.approx(r["flop_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e12, rel=1e-3)
+    assert r["traffic"] is None or r["traffic"] > 0
+    c = d["cpu_baseline"]
+    assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0
+    assert c["unit"] == d["unit"] and c["sample"]
+    # the parity path rides in the same line and meets the north-star gate
+    assert d["fp32"]["mpjpe_delta_mm"] <= 1e-4
+
+
+def test_bench_cli_parses():
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    for flag in ("--gpus", "--steps", "--warmup", "--global-batch", "--traj", "--stream"):
+        assert flag in out.stdout, flag
