@@ -631,7 +631,7 @@ def windows_main(args, world, rank, dev):
     K.E + window gather + camera concat inside the step."""
     from common.models.TemporalModel import TemporalModelOptimized1f
     from vp3d_amd import synth
-    from vp3d_amd.shard import shard_range
+    from vp3d_amd.shard import window_shard
 
     traj = args.traj
     dtype = args.dtype or ("fp16" if traj else "bf16")
@@ -647,13 +647,12 @@ def windows_main(args, world, rank, dev):
     if args.batch:
         G = args.batch * world
         s, e = rank * args.batch, (rank + 1) * args.batch
+        pairs = torch.from_numpy(pool.global_pairs(G)[s:e]).to(dev)
         scaling = "weak"
     else:
         G = args.global_batch
-        s, e = shard_range(G, rank, world)
+        pairs, s, e = window_shard(pool, G, rank, world, dev)
         scaling = "strong"
-    pairs_all = pool.global_pairs(G)
-    pairs = torch.from_numpy(pairs_all[s:e]).to(dev)
     B = e - s
     lifter = model.native_lifter(dev)
     lifter.reserve(B, RF, dtype)

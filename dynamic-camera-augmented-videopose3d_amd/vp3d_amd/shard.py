@@ -42,6 +42,16 @@ def time_shard(T_out: int, rank: int, world: int, receptive_field: int) -> Tuple
     return o0, o1, o0, o1 + receptive_field - 1
 
 
+def window_shard(pool, G: int, rank: int, world: int, device) -> Tuple[torch.Tensor, int, int]:
+    """This rank's slice of a global window set of G (sequence, start) pairs drawn from
+    `pool` (vp3d_amd.pipeline.SyntheticWindowPool or anything with global_pairs(G)):
+    the pair rows [s, e) on `device`, and s, e.  The config-4 bench and its multi-rank
+    GPU test shard through this one function."""
+    s, e = shard_range(G, rank, world)
+    pairs_all = pool.global_pairs(G)
+    return torch.from_numpy(pairs_all[s:e]).to(device), s, e
+
+
 def forward_sharded_windows(fn: Callable[[torch.Tensor], torch.Tensor], windows: torch.Tensor,
                             rank: int, world: int) -> torch.Tensor:
     """Run `fn` on this rank's contiguous shard of a (B, T, J, F) window batch."""

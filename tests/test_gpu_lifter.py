@@ -74,25 +74,45 @@ def test_opt1f_243_h16_large_batch(dtype):
     _check(y, ref, gt, dtype)
 
 
-def test_opt1f_outputs_past_2gb_bf16():
-    """B = 40,000 windows: the block-1 outputs are 2.2 GB (past 2^31 bytes: the q64
-    kernel's per-tile output resource) and the expand output 6.6 GB.  The input is 64
-    distinct windows tiled 625 times, so every output window is checked against the
-    oracle (windows are independent in the strided model)."""
-    model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024, seed=0)
-    xs = synth.normalized_windows(1, "x64_243", 64, 243)
-    ref = lifter_forward(sd, xs, [3, 3, 3, 3, 3], strided=True).numpy()
-    x = np.ascontiguousarray(np.tile(xs, (625, 1, 1, 1)))
-    model.cuda().set_compute_dtype("bf16")
+_CONFIG4 = {}
+
+
+def _config4_ref():
+    if not _CONFIG4:
+        model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024, seed=0)
+        xs = synth.normalized_windows(1, "x64_243", 64, 243)
+        _CONFIG4.update(model=model, xs=xs,
+                        ref=lifter_forward(sd, xs, [3, 3, 3, 3, 3], strided=True).numpy())
+    return _CONFIG4["model"], _CONFIG4["xs"], _CONFIG4["ref"]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_config4_b65536(dtype):
+    """Config 4's whole global batch on one GPU: B = 65,536 windows (243 frames, 1024 ch),
+    the shape the headline bench times.  The block-1 outputs are 3.6 GB in bf16 (past 2^31
+    bytes: the q64 kernel's per-tile output resource) and 7.2 GB in fp32; the expand output
+    10.9 / 21.7 GB.  The input is the 64 oracle windows tiled 1,024 times (windows are
+    independent in the strided model), so the first, middle and last tiles -- the last
+    256-row tiles of every layer -- are checked against the oracle, and every window
+    against the tolerance."""
+    model, xs, ref = _config4_ref()
+    reps = 65536 // 64
+    x = torch.from_numpy(xs).cuda().repeat(reps, 1, 1, 1)
+    model.cuda().set_compute_dtype(dtype)
     with torch.no_grad():
-        y = model(torch.from_numpy(x).cuda())
+        y = model(x)
     torch.cuda.synchronize()
-    y = y.cpu().numpy().reshape((625,) + ref.shape)
     del x
+    assert y.shape == (65536, 1, 17, 3)
+    y = y.cpu().numpy().reshape((reps,) + ref.shape)
     gt = synth.gt_poses(3, "gt", 64 * ref.shape[1], 17).reshape(ref.shape)
-    for r in (0, 1, 311, 623, 624):  # first, middle and last copies (last tiles of every layer)
-        _check(y[r], ref, gt, "bf16")
-    assert np.abs(y - ref[None]).max() <= H16_TOL["bf16"][0]
+    for r in (0, 1, reps // 2, reps - 2, reps - 1):
+        _check(y[r], ref, gt, dtype)
+    tol = FP32_COORD_TOL if dtype == "fp32" else H16_TOL[dtype][0]
+    assert np.abs(y - ref[None]).max() <= tol
+    if dtype == "fp32":
+        # tiles of identical windows: the same rows of every tile give the same bits
+        assert np.array_equal(y[0], y[reps - 1])
 
 
 @pytest.mark.parametrize("gemm,opt1f", [("big", True), ("8p", True), ("8p", False), ("q64", False),
