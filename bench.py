@@ -41,7 +41,9 @@ METRIC = "3D poses/sec, 243-frame RF, 17 joints, 1024ch; MPJPE vs ref"
 FW = [3, 3, 3, 3, 3]
 CHANNELS = 1024
 JOINTS = 17
-PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+# MI355X dense peaks (MI355X_MICROARCH.md); f16x3 (split fp16) issues three f16 MFMA products
+# per algorithmic multiply-add, so its algorithmic-FLOP ceiling is the f16 peak / 3
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3, "f16x3": 2500.0 / 3}
 
 
 def parse():
@@ -54,8 +56,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=None,
                     help="windows per GPU per step instead of --global-batch (weak scaling); the per-step "
                          "unit count of --train / --sequence / --seq-model")
-    ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32"],
-                    help="bf16 (configs 2/4), fp16 (--traj, --stream)")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32", "f16x3"],
+                    help="bf16 (configs 2/4), fp16 (--traj, --stream); f16x3 = split fp16 (fp32-level "
+                         "accuracy on the 16-bit MFMAs)")
     ap.add_argument("--sweep", type=lambda v: [int(t) for t in v.split(",") if t], default=[1024, 8192, 65536],
                     help="config-2 batch sweep on one GPU (windows per step)")
     ap.add_argument("--no-extras", action="store_true", help="skip the fp32 leg, the sweep and the CPU baseline")
@@ -741,22 +744,27 @@ def windows_main(args, world, rank, dev):
 
     if world == 1 and not args.no_extras:
         with torch.no_grad():
-            # ---- fp32 parity path: same windows, same B, fewer steps ----
+            # ---- the parity-gate paths: exact fp32 and split fp16 (f16x3), same windows and B ----
             if not traj:
-                y32 = torch.empty_like(y)
-                lifter.reserve(B, RF, "fp32")
-                k32 = max(3, args.steps // 4)
-                dt32, pl32, dom32 = profiled_run(lifter, make_step("fp32", x, pairs, y32), k32, 1, 0.3, 1)
-                v32 = G * k32 / dt32
-                y32s = y32[idx].cpu().numpy()
-                out["fp32"] = {"value": round(v32, 2), "unit": "poses/s", "steps": k32,
-                               "ms_per_step": round(dt32 / k32 * 1e3, 4),
-                               "roofline": roofline_of(dom32, PEAK_TFLOPS["fp32"]),
-                               "per_layer_ms": pl32,
-                               "mpjpe_delta_mm": abs(mp(y32s) - mp(ref)) * 1e3,
-                               "max_coord_delta_mm": float(np.abs(y32s - ref).max()) * 1e3}
-                parity["fp32_mpjpe_delta_mm"] = out["fp32"]["mpjpe_delta_mm"]
-                parity["fp32_max_coord_delta_mm"] = out["fp32"]["max_coord_delta_mm"]
+                for dt_acc, ksteps in (("fp32", max(3, args.steps // 4)), ("f16x3", max(5, args.steps // 2))):
+                    if dt_acc == dtype:
+                        continue
+                    ya = torch.empty_like(y)
+                    lifter.reserve(B, RF, dt_acc)
+                    dta, pla, doma = profiled_run(lifter, make_step(dt_acc, x, pairs, ya), ksteps, 1, 0.3, 1)
+                    yas = ya[idx].cpu().numpy()
+                    out[dt_acc] = {"value": round(G * ksteps / dta, 2), "unit": "poses/s", "steps": ksteps,
+                                   "ms_per_step": round(dta / ksteps * 1e3, 4),
+                                   "roofline": roofline_of(doma, PEAK_TFLOPS[dt_acc]),
+                                   "per_layer_ms": pla,
+                                   "mpjpe_delta_mm": abs(mp(yas) - mp(ref)) * 1e3,
+                                   "max_coord_delta_mm": float(np.abs(yas - ref).max()) * 1e3}
+                    parity[f"{dt_acc}_mpjpe_delta_mm"] = out[dt_acc]["mpjpe_delta_mm"]
+                    parity[f"{dt_acc}_max_coord_delta_mm"] = out[dt_acc]["max_coord_delta_mm"]
+                    del ya
+                if "f16x3" in out:
+                    out["f16x3"]["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per "
+                                                            "algorithmic multiply-add (hi.hi + hi.lo + lo.hi)")
                 # ---- config-2 batch sweep (1 GPU) ----
                 sweep = {}
                 for Bs in args.sweep:
@@ -780,8 +788,9 @@ def windows_main(args, world, rank, dev):
                                f"{int(xc.shape[0])})", target_s=args.cpu_seconds / 5)
             out["cpu_baseline"] = cpu
             out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
-            if "fp32" in out:
-                out["fp32"]["speedup_vs_cpu"] = round(out["fp32"]["value"] / cpu["value"], 1)
+            for dt_acc in ("fp32", "f16x3"):
+                if dt_acc in out:
+                    out[dt_acc]["speedup_vs_cpu"] = round(out[dt_acc]["value"] / cpu["value"], 1)
     print(json.dumps(out), flush=True)
 
 

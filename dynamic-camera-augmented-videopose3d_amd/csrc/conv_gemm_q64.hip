@@ -72,7 +72,14 @@ __device__ int g_stagger_iters;
 __device__ int g_stagger_groups;
 #endif
 
-template <typename CT, int EPI = 0>
+// X3 (split fp16, VP3D_DTYPE_F16X3): A and W rows hold every f32 value x as two f16
+// halves hi = f16(x), lo = f16(x - hi), each 32-wide K group stored [hi(32) | lo(32)] --
+// exactly a 16-bit operand of twice the K -- so the DMA, LDS layout and fragment reads
+// are the plain kernel's, with kh = 0 the hi and kh = 1 the lo fragments of 32 K values.
+// The MFMA pattern per fragment pair is hi.hi + hi.lo + lo.hi (the lo.lo term, 2^-22
+// relative, is dropped): 3 MFMAs per 2 fragment reads instead of 2.
+// X3 = 1: split output rows; X3 = 2: f32 output rows (the layer before the shrink).
+template <typename CT, int EPI = 0, int X3 = 0>
 __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
 #ifdef VP3D_ABLATION
     if (g_stagger_iters > 0 && blockIdx.x < 256) {
@@ -94,7 +101,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
         s_shift[i] = p.shift[i];
     }
 
-    const int ntn = p.N / QN;
+    const int ntn = (p.N + QN - 1) / QN;  // X3: N % 64 == 0, waves past N skip the epilogue
     const int ntm = (p.M + QM - 1) / QM;
     const int wg = xcd_remap(blockIdx.x, ntm * ntn);
     const int tile_m = wg / ntn;
@@ -187,14 +194,27 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
     };
     auto mma = [&](int h, int g) {
         __builtin_amdgcn_s_setprio(1);
+        if constexpr (X3 != 0) {
+            // term t: (W, A) halves (hi, hi), (hi, lo), (lo, hi); 8 independent
+            // accumulators between two MFMAs on the same one
 #pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
+            for (int t = 0; t < 3; ++t)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int jj = 0; jj < 2; ++jj)
-                    acc[4 * h + i][2 * g + jj] =
-                        mfma16<CT>(bf[g][jj][kh], af[i][kh], acc[4 * h + i][2 * g + jj]);
+                    for (int jj = 0; jj < 2; ++jj)
+                        acc[4 * h + i][2 * g + jj] = mfma16<CT>(bf[g][jj][t == 2 ? 1 : 0], af[i][t == 1 ? 1 : 0],
+                                                                acc[4 * h + i][2 * g + jj]);
+        } else {
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj)
+                        acc[4 * h + i][2 * g + jj] =
+                            mfma16<CT>(bf[g][jj][kh], af[i][kh], acc[4 * h + i][2 * g + jj]);
+        }
         __builtin_amdgcn_s_setprio(0);
     };
     auto compute_seg = [&](int h, int g) {
@@ -253,6 +273,19 @@ __global__ __launch_bounds__(512, 1) void conv_gemm_q64(ConvGemmParams p) {
     }
     if (wr == 0) qbarrier();  // match group 1's extra barrier
 
+    if constexpr (X3 != 0) {
+        if (n0 + wc * 64 >= p.N) return;  // a wave's 64 channels lie wholly past N
+        constexpr int OB = X3 == 2 ? 4 : 2;  // output element bytes
+        const size_t y_rest = (size_t)(p.M - m0) * p.ldy * OB;
+        const __amdgpu_buffer_rsrc_t y_rsrc =
+            make_rsrc((const char*)p.Y + (size_t)m0 * p.ldy * OB,
+                      (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+        if (p.R)
+            epilogue_tp_x3<X3 == 2, 1>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc, m0);
+        else
+            epilogue_tp_x3<X3 == 2, 0>(p, acc, m0 + wr * 128, n0 + wc * 64, lane, s_scale, s_shift, y_rsrc, m0);
+        return;
+    }
     // the output resource starts at the tile's first row (outputs past 2^31 bytes: the
     // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
     const size_t y_rest = (size_t)(p.M - m0) * p.ldy * sizeof(CT);
@@ -289,6 +322,24 @@ bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, A
     // any output size: the store resource is rebased per tile, A / W / residual
     // addresses are 64-bit (A rows and Np * Kp stay below 2^31)
     return (size_t)p.N * p.Kp < (1u << 31);
+}
+
+bool conv_gemm_q64_x3_eligible(const ConvGemmParams& p, bool out_f32) {
+    if (p.Ktap % QK != 0 || p.Kp % QK != 0 || p.lda % 8 != 0) return false;
+    if (p.N % 64 != 0 || p.N > QMAXN || p.ldy % (out_f32 ? 4 : 8) != 0 || (p.R && p.ldr % 8 != 0)) return false;
+    if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
+        (reinterpret_cast<uintptr_t>(p.W) & 15) || (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
+        return false;
+    return (size_t)((p.N + QN - 1) / QN * QN) * p.Kp < (1u << 31);
+}
+
+hipError_t launch_conv_gemm_q64_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream) {
+    const dim3 grid(((p.M + QM - 1) / QM) * ((p.N + QN - 1) / QN));
+    if (out_f32)
+        hipLaunchKernelGGL((conv_gemm_q64<_Float16, 0, 2>), grid, dim3(512), 0, stream, p);
+    else
+        hipLaunchKernelGGL((conv_gemm_q64<_Float16, 0, 1>), grid, dim3(512), 0, stream, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream) {

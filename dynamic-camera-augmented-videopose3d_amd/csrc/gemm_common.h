@@ -392,5 +392,100 @@ __device__ __forceinline__ void epilogue_tp(const ConvGemmParams& p, f32x4 (&acc
     }
 }
 
+// epilogue_tp for the split-fp16 path (VP3D_DTYPE_F16X3, conv_gemm_q64<_, _, X3>): rows of
+// split activations hold channel n's halves at 64 (n / 32) + n % 32 (hi) and +32 (lo), so
+// a lane's 8 channels nw + 32 jp + c0 + 0..7 are 16 bytes of hi and, 64 bytes on, 16 of lo.
+// Residual (block input, split): hi + lo rebuilt in f32 and added as one value (the
+// reference's res + relu(bn(conv)), TemporalModel.py:135,195).  Output: split (hi =
+// f16(v), lo = f16(v - hi)) or, OUT_F32, the f32 row for the exact f32 shrink GEMM.
+// 4 residual loads and 4 stores per row block: the waits count both.
+template <bool OUT_F32, int HAS_R>
+__device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&acc)[8][4], int mw, int nw, int lane,
+                                               const float* s_scale, const float* s_shift,
+                                               __amdgpu_buffer_rsrc_t y_rsrc, int m_base) {
+    constexpr int MI = 8;
+    const int grp = lane >> 4;
+    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+    float sc[4][4], sh[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = nw + 16 * j + 4 * grp;
+        const f32x4 s4 = *(const f32x4*)&s_scale[n];
+        const f32x4 h4 = *(const f32x4*)&s_shift[n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            sc[j][q] = s4[q];
+            sh[j][q] = h4[q];
+        }
+    }
+    u32x4 res[2][2][2];  // [row block parity][jp][hi, lo]
+    auto load_res = [&](int i, u32x4 (&rr)[2][2]) {
+        int m = mw + i * 16 + (lane & 15);
+        m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
+        const f16* rp = (const f16*)p.R + (int64_t)res_row(p, m) * p.ldr + 2 * nw + c0;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+            rr[jp][0] = *(const u32x4*)(rp + 64 * jp);
+            rr[jp][1] = *(const u32x4*)(rp + 64 * jp + 32);
+        }
+    };
+    if (HAS_R) load_res(0, res[0]);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int m = mw + i * 16 + (lane & 15);
+        if (HAS_R) {
+            // issue order per block: res(i+1) (4 loads), [wait res(i)], stores(i) (4)
+            if (i + 1 < MI) load_res(i + 1, res[(i + 1) & 1]);
+            if (i == 0)
+                vm_wait_n<4>();
+            else if (i + 1 < MI)
+                vm_wait_n<8>();
+            else
+                vm_wait_n<4>();
+        }
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+            float v[8];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                float x = __fadd_rn(__fmul_rn(acc[i][2 * jp][d], sc[2 * jp][d]), sh[2 * jp][d]);
+                float y = __fadd_rn(__fmul_rn(acc[i][2 * jp + 1][d], sc[2 * jp + 1][d]), sh[2 * jp + 1][d]);
+                if (p.relu) {
+                    x = x > 0.f ? x : 0.f;
+                    y = y > 0.f ? y : 0.f;
+                }
+                asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+                v[d] = x;
+                v[d + 4] = y;
+            }
+            if (HAS_R) {
+                const f16x8 rh = __builtin_bit_cast(f16x8, res[i & 1][jp][0]);
+                const f16x8 rl = __builtin_bit_cast(f16x8, res[i & 1][jp][1]);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += (float)rh[e] + (float)rl[e];
+            }
+            const bool in = m < p.M;
+            if constexpr (OUT_F32) {
+                const uint32_t yo = in ? (uint32_t)(((size_t)(m - m_base) * p.ldy + nw + 32 * jp + c0) * 4) : 0xFFFFFFE0u;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}),
+                                                       y_rsrc, yo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[4], v[5], v[6], v[7]}),
+                                                       y_rsrc, yo + 16, 0, 0);
+            } else {
+                f16x8 oh, ol;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    oh[e] = (f16)v[e];
+                    ol[e] = (f16)(v[e] - (float)oh[e]);
+                }
+                const uint32_t yo = in ? (uint32_t)(((size_t)(m - m_base) * p.ldy + 2 * nw + 64 * jp + c0) * 2)
+                                       : 0xFFFFFF00u;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, oh), y_rsrc, yo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ol), y_rsrc, yo + 64, 0, 0);
+            }
+        }
+    }
+}
+
 }  // namespace gemm
 }  // namespace vp3d

@@ -53,6 +53,10 @@ inline float f16_to_f32(uint16_t h) {
     return (float)v;
 }
 
+// Position of element k (of a K-wide f32 row) in its split-fp16 row of 2K halves:
+// 32-wide groups stored [hi(32) | lo(32)] (lo at +32).
+inline size_t x3_pos(size_t k) { return (k >> 5) * 64 + (k & 31); }
+
 // One convolution of the stack (expand, k-conv / 1x1 of each block, shrink).
 struct Layer {
     int cin = 0, cout = 0, taps = 1, dil = 1, stride = 1;  // conv geometry
@@ -70,6 +74,11 @@ struct Layer {
     // kernel's loader feeds them 1.0); null when K + 2 does not fit in Kp
     uint16_t* wfbf = nullptr;
     uint16_t* wfh = nullptr;
+    // split-fp16 path (VP3D_DTYPE_F16X3, every layer but the shrink): the f32 weights
+    // scaled by 2^e (max |W 2^e| in [2^14, 2^15)) and carried as hi + lo f16 halves,
+    // [Np][2 Kp] with each 32-wide K group stored [hi(32) | lo(32)]; scale_x3 = scale * 2^-e
+    uint16_t* wx3 = nullptr;
+    float* scale_x3 = nullptr;
 };
 
 struct ProfEvent {

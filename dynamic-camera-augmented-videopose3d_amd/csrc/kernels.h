@@ -53,6 +53,11 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
 // 64-deep K-tiles staged as whole 128-byte lines, quadrant phases (conv_gemm_q64.hip).
 bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream);
+// Split-fp16 mode of conv_gemm_q64 (VP3D_DTYPE_F16X3): A / W / residual rows of f16 halves,
+// each 32-wide K group [hi(32) | lo(32)] (Ktap, Kp, lda, ldr in halves); output split
+// (ldy halves) or, out_f32, f32 rows (ldy floats).  N % 64 == 0, N <= 1024.
+bool conv_gemm_q64_x3_eligible(const ConvGemmParams& p, bool out_f32);
+hipError_t launch_conv_gemm_q64_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream);
 // measurement only (VP3D_ABL=7 launches): 10 u64 timestamps/ids per workgroup
 hipError_t conv_gemm_8p_set_trace(unsigned long long* buf);
 
@@ -109,6 +114,17 @@ hipError_t launch_stream_gemv(const StreamLayerParams& q, Act wtype, hipStream_t
 // workgroup g owns channels [g*CPW, (g+1)*CPW) of every layer with their 16-bit weights
 // resident in LDS, the layer outputs handed to every workgroup through {tag, value}
 // granules.  Layers: 0 = expand, 2b-1 / 2b = block b's k-conv / 1x1, nl-1 = shrink.
+// Bounded-spin fault state of the persistent stream kernels: `err` (device, sticky until
+// vp3d_stream_reset) makes every later launch a no-op, `err_host` (host-mapped) lets the
+// host refuse further steps without a synchronisation; spin_ticks = the 100 MHz-clock
+// budget of one wait (VP3D_STREAM_SPIN_TICKS overrides it: fault-injection tests).
+struct StreamFault {
+    unsigned* err;
+    unsigned* err_host;
+    unsigned long long spin_ticks;
+};
+constexpr unsigned long long kStreamSpinTicks = 25000000ull;  // 0.25 s
+
 constexpr int kStreamMaxLayers = 16;
 constexpr int kStreamMaxTaps = 8;
 constexpr int kStreamMaxBlocks = 7;
@@ -127,7 +143,7 @@ struct StreamPersistParams {
     float* poses;                          // pose ring (queue slots of N[nl-1] floats)
     int* frames_seen;                      // stream position (read at start, advanced at the end)
     unsigned long long* gran;              // [2nb+1 edges][2 parities][C] granules, zeroed per launch
-    unsigned* err;                         // timeout word, zeroed per launch
+    StreamFault fault;                     // sticky timeout word (not zeroed per launch)
     float* state;                          // [G][state_floats]: partial-sum rings + frame history
     int steps;
 };
@@ -157,7 +173,7 @@ struct StreamPipeParams {
     int* frames_seen;                      // stream position (read at start, advanced by the last workgroup)
     unsigned* arrivals;                    // end-of-launch arrival counter (zero between launches)
     unsigned long long* gran;              // [queue][2nb+1 edges][C] granules
-    unsigned* err;                         // sticky timeout word
+    StreamFault fault;                     // sticky timeout word
     float* state;                          // [workgroups][state_stride]: k-conv rings / expand history
     int state_stride;
     int steps;
@@ -180,6 +196,12 @@ hipError_t launch_gather_windows(const float* kps, int f2, const float* cams,
                                  float* out, hipStream_t s);
 hipError_t launch_pack_rows(const float* x, int M, int T_out, int T_in, int stride, int lda,
                             int K, int Kp, void* out, bool bf16, hipStream_t s);
+// The expand conv's GEMM rows in split-fp16 form: row m = (b, t) is the K = taps * cin f32
+// values starting at frame t * stride of window b (x: (B, T_in, cin) rows, or gathered from
+// the sequences of `g` when x is null), zero padded to Kp and stored as 2 Kp halves
+// (32-wide groups [hi | lo]).
+hipError_t launch_pack_rows_x3(const float* x, const struct GatherSrc* g, int M, int T_out, int T_in, int stride,
+                               int cin, int K, int Kp, void* out, hipStream_t s);
 hipError_t launch_mpjpe_accumulate(const float* pred, const float* target, int64_t n,
                                    double* acc, hipStream_t s);
 hipError_t launch_mpjpe_backward(const float* pred, const float* target, int64_t n, const float* grad_loss,

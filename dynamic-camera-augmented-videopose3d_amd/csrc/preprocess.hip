@@ -296,7 +296,74 @@ __global__ void pack_rows_kernel(const float* __restrict__ x, int M, int T_out, 
     }
 }
 
+// Split-fp16 expand rows (VP3D_DTYPE_F16X3): 8 K values per thread -> 16 B of hi and,
+// 64 B further, 16 B of lo.  With `pairs` the frames come straight from the sequences,
+// edge-clamped per sequence as gather_windows_kernel (generators.py:92-137), each
+// frame = [kps (f2) | cams (12)] (CamTransformer.py:187-190).
+__global__ void pack_rows_x3_kernel(const float* __restrict__ x, const float* __restrict__ kps, int f2,
+                                    const float* __restrict__ cams, const int64_t* __restrict__ seq_off,
+                                    const int32_t* __restrict__ seq_len, const int32_t* __restrict__ pairs,
+                                    int lead, int M, int T_out, int T_in, int stride, int cin, int K, int Kp,
+                                    _Float16* __restrict__ out) {
+    const int chunks = Kp >> 3;
+    const int64_t total = (int64_t)M * chunks;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int m = (int)(i / chunks);
+        const int c = (int)(i - (int64_t)m * chunks) * 8;
+        const int b = m / T_out;
+        const int t = m - b * T_out;
+        float v[8];
+        if (pairs) {
+            const int seq = pairs[2 * b];
+            const int len = seq_len[seq];
+            const int f0 = pairs[2 * b + 1] - lead + t * stride;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = c + e;
+                v[e] = 0.f;
+                if (k < K) {
+                    const int tap = k / cin;
+                    const int ch = k - tap * cin;
+                    int f = f0 + tap;
+                    f = f < 0 ? 0 : (f >= len ? len - 1 : f);
+                    const int64_t frame = seq_off[seq] + f;
+                    v[e] = ch < f2 ? kps[frame * f2 + ch] : cams[frame * 12 + (ch - f2)];
+                }
+            }
+        } else {
+            const float* row = x + ((int64_t)b * T_in + (int64_t)t * stride) * cin;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = c + e < K ? row[c + e] : 0.f;
+        }
+        typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+        h8 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            hi[e] = (_Float16)v[e];
+            lo[e] = (_Float16)(v[e] - (float)hi[e]);
+        }
+        _Float16* o = out + (int64_t)m * 2 * Kp + (c >> 5) * 64 + (c & 31);
+        *(h8*)o = hi;
+        *(h8*)(o + 32) = lo;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_pack_rows_x3(const float* x, const GatherSrc* g, int M, int T_out, int T_in, int stride,
+                               int cin, int K, int Kp, void* out, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    const dim3 grid = grid_for((int64_t)M * (Kp / 8), 4);
+    if (g)
+        hipLaunchKernelGGL(pack_rows_x3_kernel, grid, dim3(kThreads), 0, s, nullptr, g->kps, g->f2, g->cams,
+                           g->seq_off, g->seq_len, g->pairs, g->lead, M, T_out, T_in, stride, cin, K, Kp,
+                           (_Float16*)out);
+    else
+        hipLaunchKernelGGL(pack_rows_x3_kernel, grid, dim3(kThreads), 0, s, x, nullptr, 0, nullptr, nullptr,
+                           nullptr, nullptr, 0, M, T_out, T_in, stride, cin, K, Kp, (_Float16*)out);
+    return hipGetLastError();
+}
 
 hipError_t launch_pack_rows(const float* x, int M, int T_out, int T_in, int stride, int lda,
                             int K, int Kp, void* out, bool bf16, hipStream_t s) {

@@ -23,7 +23,7 @@
 //
 // Per step: 9 hand-off edges (expand out, then per block the k-conv and 1x1 outputs);
 // the shrink runs on the few CUs that own its 51 rows.  Every spin is bounded (~0.25 s
-// of the 100 MHz clock); a timeout sets the launch's error word and every wave leaves.
+// of the 100 MHz clock); a timeout sets the sticky error word and every wave leaves.
 #include <stdint.h>
 
 #include "kernels.h"
@@ -38,7 +38,6 @@ typedef __attribute__((address_space(1))) unsigned int gu32;
 constexpr int kThreads = 256;
 constexpr int kWaves = 4;
 constexpr int kLds = 156 * 1024;  // one workgroup per CU
-constexpr unsigned long long kSpinTicks = 25000000ull;  // 0.25 s of the 100 MHz clock
 
 __device__ __forceinline__ float wave_sum(float s) {
 #pragma unroll
@@ -81,10 +80,10 @@ __device__ __forceinline__ void publish(gu64* g, unsigned epoch, float v) {
 
 // Sweep the C granules of one edge into LDS: every thread owns granules tid + j*256,
 // polls the ones still missing (four loads in flight per pass), and returns true once
-// every tag matched; false on timeout (sets the launch's error word) or when another
+// every tag matched; false on timeout (sets the sticky error word) or when another
 // wave of the workgroup aborted.
 __device__ __forceinline__ bool sweep(gu64* g, int C, unsigned epoch, float* x, volatile int* abort_flag,
-                                      unsigned* err, int tid) {
+                                      const StreamFault& f, int tid) {
     const unsigned long long start = __builtin_amdgcn_s_memrealtime();
     for (int i0 = tid; i0 < C; i0 += 4 * kThreads) {
         unsigned pending = 0;
@@ -106,9 +105,10 @@ __device__ __forceinline__ bool sweep(gu64* g, int C, unsigned epoch, float* x, 
                 }
             if (!pending) break;
             if (*abort_flag) return false;
-            if (__builtin_amdgcn_s_memrealtime() - start > kSpinTicks) {
+            if (__builtin_amdgcn_s_memrealtime() - start > f.spin_ticks) {
                 *abort_flag = 1;
-                __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gu32*)f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (f.err_host) __hip_atomic_store(f.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return false;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -125,6 +125,9 @@ __global__ __launch_bounds__(kThreads, 1) void stream_persist_kernel(StreamPersi
     const int wg = blockIdx.x;
     const int C = p.C, CPW = p.CPW, nb = p.nb, cin0 = p.cin0;
     const int c0 = wg * CPW;
+    // a stream that timed out stays failed until vp3d_stream_reset: no-op launches, so the
+    // frame position and the partial-sum rings never drift out of step
+    if (__hip_atomic_load(p.fault.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     if (tid == 0) abort_flag = 0;
 
     // ---- LDS carve (byte offsets precomputed on the host, all 16-byte aligned) ----
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_persist_kernel(StreamPersi
             const int lk = 2 * b - 1, lp = 2 * b;
             const int d = p.dil[b], R = p.ring[b];
             // x_b(t) from every CU
-            if (!sweep(edge(2 * b - 2), C, epoch, xbuf, &abort_flag, p.err, tid)) abort_flag = 1;
+            if (!sweep(edge(2 * b - 2), C, epoch, xbuf, &abort_flag, p.fault, tid)) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
             if (wid < CPW) {
@@ -249,7 +252,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_persist_kernel(StreamPersi
             ring_base += R;
             __syncthreads();  // xbuf is overwritten by the next sweep
             // h_b(t) from every CU
-            if (!sweep(edge(2 * b - 1), C, epoch, xbuf, &abort_flag, p.err, tid)) abort_flag = 1;
+            if (!sweep(edge(2 * b - 1), C, epoch, xbuf, &abort_flag, p.fault, tid)) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
             if (wid < CPW) {
@@ -263,7 +266,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_persist_kernel(StreamPersi
         }
         // ---- shrink on the workgroups that own its rows ----
         if (wg < nsh) {
-            if (!sweep(edge(2 * nb), C, epoch, xbuf, &abort_flag, p.err, tid)) abort_flag = 1;
+            if (!sweep(edge(2 * nb), C, epoch, xbuf, &abort_flag, p.fault, tid)) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
             const int ls = p.nl - 1;

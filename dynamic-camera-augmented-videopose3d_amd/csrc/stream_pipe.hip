@@ -46,7 +46,6 @@ typedef __attribute__((address_space(1))) unsigned int gu32;
 
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
-constexpr unsigned long long kSpinTicks = 25000000ull;  // 0.25 s of the 100 MHz clock
 
 // 16-bit weight halves of a packed u32 -> f32 (exact)
 template <typename WT>
@@ -92,7 +91,7 @@ __device__ __forceinline__ void pref_issue(Pref& r, const gu64* g, int n, int ti
 }
 
 __device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* x, volatile int* abort_flag,
-                            unsigned* err, int tid) {
+                            const StreamFault& f, int tid) {
     unsigned pending = 0;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -110,9 +109,10 @@ __device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* 
             start = __builtin_amdgcn_s_memrealtime();
         } else {
             if (*abort_flag) return false;
-            if (__builtin_amdgcn_s_memrealtime() - start > kSpinTicks) {
+            if (__builtin_amdgcn_s_memrealtime() - start > f.spin_ticks) {
                 *abort_flag = 1;
-                __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gu32*)f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (f.err_host) __hip_atomic_store(f.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 return false;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -219,6 +219,9 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         if (l == nl - 1) Nout = p.N[l];
     }
     if (role < 0) return;
+    // a stream that timed out stays failed until vp3d_stream_reset: no-op launches (no
+    // arrival, no position advance), so nothing drifts out of step
+    if (__hip_atomic_load(p.fault.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     K0 = p.Kp[0];
     const int c_lo = (int)((int64_t)N * gi / gn), c_hi = (int)((int64_t)N * (gi + 1) / gn);
     const bool is_expand = role == 0, is_shrink = role == nl - 1;
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         for (int s = 0; s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
-            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid)) abort_flag = 1;
+            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid)) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
             if (s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
@@ -407,8 +410,8 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
             float* rv = rbuf + (s & 1) * kPipeMaxCh;
-            bool ok = pref_finish(pr, edge(role - 2, t) + c_lo, nres, (unsigned)t + 1u, rv, &abort_flag, p.err, tid);
-            if (ok) ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.err, tid);
+            bool ok = pref_finish(pr, edge(role - 2, t) + c_lo, nres, (unsigned)t + 1u, rv, &abort_flag, p.fault, tid);
+            if (ok) ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid);
             if (!ok) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;

@@ -166,10 +166,14 @@ void free_layers(vp3d_handle* h) {
         hipFree(L.shift);
         hipFree(L.wfbf);
         hipFree(L.wfh);
+        hipFree(L.wx3);
+        hipFree(L.scale_x3);
         L.w32 = nullptr;
         L.wbf = L.wh = nullptr;
         L.scale = L.shift = nullptr;
         L.wfbf = L.wfh = nullptr;
+        L.wx3 = nullptr;
+        L.scale_x3 = nullptr;
     }
 }
 
@@ -251,6 +255,30 @@ int upload_weights(vp3d_handle* h, const float* const* w, int n) {
             HIP_TRY(hipMemcpy(L.wfbf, fbf.data(), fbf.size() * 2, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(L.wfh, fh.data(), fh.size() * 2, hipMemcpyHostToDevice));
         }
+        if (!is_shrink) {
+            // split-fp16 copy: W 2^e = hi + lo, both f16 (hi = f16(W 2^e), lo = f16(W 2^e - hi)),
+            // the power of two undone exactly by the epilogue scale
+            float wmax = 0.f;
+            for (float v : p32) wmax = std::max(wmax, std::fabs(v));
+            const int e = wmax > 0.f ? 14 - (int)std::floor(std::log2((double)wmax)) : 0;
+            std::vector<uint16_t> px3((size_t)L.Np * 2 * L.Kp, 0);
+            for (int o = 0; o < L.cout; ++o)
+                for (int k = 0; k < L.Kp; ++k) {
+                    const float v = std::ldexp(p32[(size_t)o * L.Kp + k], e);
+                    const uint16_t hi = f32_to_f16_rne(v);
+                    const size_t q = (size_t)o * 2 * L.Kp + x3_pos(k);
+                    px3[q] = hi;
+                    px3[q + 32] = f32_to_f16_rne(v - f16_to_f32(hi));
+                }
+            std::vector<float> scx3(L.cout);
+            for (int o = 0; o < L.cout; ++o) scx3[o] = std::ldexp(sc[o], -e);
+            if (!L.wx3) {
+                HIP_TRY(hipMalloc(&L.wx3, px3.size() * 2));
+                HIP_TRY(hipMalloc(&L.scale_x3, L.cout * 4));
+            }
+            HIP_TRY(hipMemcpy(L.wx3, px3.data(), px3.size() * 2, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(L.scale_x3, scx3.data(), L.cout * 4, hipMemcpyHostToDevice));
+        }
     }
     return VP3D_OK;
 }
@@ -307,7 +335,8 @@ bool layer_lengths(const vp3d_handle* h, int T, std::vector<int>& len) {
     return layer_lengths(h->cfg, h->pad, h->layers, T, len);
 }
 
-size_t esize(int dtype) { return dtype == VP3D_DTYPE_F32 ? 4 : 2; }
+// bytes per activation element: f32, one 16-bit value, or a split-fp16 (hi, lo) pair
+size_t esize(int dtype) { return dtype == VP3D_DTYPE_F32 || dtype == VP3D_DTYPE_F16X3 ? 4 : 2; }
 
 int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
     std::vector<int> len;
@@ -315,7 +344,7 @@ int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
     const size_t rows = (size_t)B * len[0];
     // three rotating activation buffers + (16-bit path) the packed expand-conv rows
     const size_t need = 3 * rows * h->cfg.channels * esize(dtype) +
-                        (dtype == VP3D_DTYPE_F32 ? 0 : rows * h->layers[0].Kp * 2);
+                        (dtype == VP3D_DTYPE_F32 ? 0 : rows * h->layers[0].Kp * (dtype == VP3D_DTYPE_F16X3 ? 4 : 2));
     if (need <= h->ws_bytes) return VP3D_OK;
     if (h->ws) HIP_TRY(hipFree(h->ws));
     h->ws = nullptr;
@@ -324,6 +353,10 @@ int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
     h->ws_bytes = need;
     return VP3D_OK;
 }
+
+// the split-fp16 path runs every conv but the shrink on conv_gemm_q64's X3 mode
+bool x3_supported(const vp3d_handle* h) { return h->cfg.channels % 64 == 0 && h->cfg.channels <= 1024; }
+const char* x3_requirement() { return "dtype f16x3 needs channels % 64 == 0 and channels <= 1024"; }
 
 hipEvent_t get_event(vp3d_handle* h) {
     if (!h->free_events.empty()) {
@@ -430,7 +463,8 @@ int vp3d_layer_count(const vp3d_handle* h) { return h ? (int)h->layers.size() : 
 int vp3d_reserve(vp3d_handle* h, int B, int T, int dtype) {
     if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
     if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
-    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    if (dtype < 0 || dtype > VP3D_DTYPE_F16X3) return fail(VP3D_ERR_ARG, "unknown dtype");
+    if (dtype == VP3D_DTYPE_F16X3 && !x3_supported(h)) return fail(VP3D_ERR_ARG, x3_requirement());
     return ensure_ws(h, B, T, dtype);
 }
 
@@ -453,6 +487,8 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
     if (rc) return rc;
 
     hipStream_t s = (hipStream_t)stream;
+    const bool x3 = dtype == VP3D_DTYPE_F16X3;
+    if (x3 && !x3_supported(h)) return fail(VP3D_ERR_ARG, x3_requirement());
     const Act act = dtype == VP3D_DTYPE_F32 ? Act::F32 : (dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16);
     const size_t es = esize(dtype);
     const size_t buf_elems = (size_t)B * len[0] * h->cfg.channels;
@@ -519,11 +555,45 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         const Act o_type = last ? Act::F32 : act;
         hipError_t e = hipSuccess;
         bool launched = false;
+        if (x3 && last) {
+            // shrink: the exact f32 GEMM over the f32 rows the layer before wrote
+            p.W = L.w32;
+            e = launch_conv_gemm(p, Act::F32, Act::F32, Act::F32, s);
+            launched = true;
+        } else if (x3) {
+            // split fp16: three 16-bit MFMA products per K group on conv_gemm_q64 (X3 mode)
+            if (first) {
+                // the expand conv's rows (window gather + camera concat fused) packed as halves
+                void* packed = base + 3 * buf_elems * es;
+                e = launch_pack_rows_x3(gs ? nullptr : x, gs, p.M, p.T_out, p.T_in, p.stride, L.cin, L.K, L.Kp,
+                                        packed, s);
+                if (e != hipSuccess) return fail(VP3D_ERR_HIP, std::string("pack: ") + hipGetErrorString(e));
+                p.A = packed;
+                p.T_in = p.T_out;
+                p.stride = 1;
+                p.dil = 1;
+                p.lda = 2 * L.Kp;
+                p.Ktap = 2 * L.Kp;
+            } else {
+                p.lda = 2 * L.cin;
+                p.Ktap = 2 * L.Ktap;
+            }
+            const bool out_f32 = li == nl - 2;
+            p.Kp = 2 * L.Kp;
+            p.W = L.wx3;
+            p.scale = L.scale_x3;
+            p.ldy = out_f32 ? L.cout : 2 * L.cout;
+            if (L.residual) p.ldr = 2 * L.cout;
+            if (!conv_gemm_q64_x3_eligible(p, out_f32)) return fail(VP3D_ERR_ARG, x3_requirement());
+            e = launch_conv_gemm_q64_x3(p, out_f32, s);
+            launched = true;
+        }
         // the expand kernel takes the BN-folded weights (Layer::wfbf / wfh)
         const void* wfold = act == Act::BF16 ? (const void*)L.wfbf : (const void*)L.wfh;
         ConvGemmParams pf = p;
         pf.W = wfold;
-        if (first && gs && act != Act::F32 && wfold && expand_gather_eligible(pf, *gs, o_type, act)) {
+        if (launched) {
+        } else if (first && gs && act != Act::F32 && wfold && expand_gather_eligible(pf, *gs, o_type, act)) {
             // the window gather (+ camera concat) fused into the expand conv's operand loads
             e = launch_expand_gemm_gather(pf, *gs, act, s);
             launched = true;
@@ -591,7 +661,7 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
     if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
     if (!x || !y) return fail(VP3D_ERR_ARG, "x / y is NULL");
     if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
-    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    if (dtype < 0 || dtype > VP3D_DTYPE_F16X3) return fail(VP3D_ERR_ARG, "unknown dtype");
     return forward_impl(h, x, B, T, y, dtype, stream, nullptr);
 }
 
@@ -601,7 +671,7 @@ int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const flo
     if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
     if (!kps || !seq_off || !seq_len || !pairs || !y) return fail(VP3D_ERR_ARG, "a device pointer is NULL");
     if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
-    if (dtype < 0 || dtype > 2) return fail(VP3D_ERR_ARG, "unknown dtype");
+    if (dtype < 0 || dtype > VP3D_DTYPE_F16X3) return fail(VP3D_ERR_ARG, "unknown dtype");
     const int cin = h->cfg.num_joints_in * h->cfg.in_features;
     if (f2 + (cams ? 12 : 0) != cin)
         return fail(VP3D_ERR_ASSERT, "frame features (" + std::to_string(f2) + (cams ? " + 12" : "") +
@@ -683,7 +753,7 @@ struct vp3d_stream {
     // persistent form (stream_persist.hip)
     bool persist = false;
     StreamPersistParams pp{};
-    void* hand = nullptr;              // [16 B: timeout word][granules], zeroed before each launch
+    void* hand = nullptr;              // granules, zeroed before each launch
     size_t hand_bytes = 0;
     float* pstate = nullptr;           // per-workgroup partial rings + frame history
     // layer-pipelined form (stream_pipe.hip): preferred over `persist` when it fits
@@ -693,11 +763,18 @@ struct vp3d_stream {
     unsigned long long* pipe_gran = nullptr;  // [queue][2nb+1][C] granules, cleared at reset
     size_t pipe_gran_bytes = 0;
     float* pipe_state = nullptr;
+    // persistent forms: host-mapped mirror of the sticky timeout word (frames_seen[3]), read
+    // by step / graph_launch without a synchronisation
+    unsigned* err_host = nullptr;
+    unsigned* err_host_dev = nullptr;
+    unsigned long long spin_ticks = kStreamSpinTicks;
 };
 
 namespace {
 
 constexpr int kQueue = 64;
+constexpr const char* kStreamFaultMsg =
+    "persistent stream step timed out waiting for another CU; the stream stays failed until vp3d_stream_reset";
 
 int pow2_at_least(int v) {
     int r = 1;
@@ -793,7 +870,7 @@ bool stream_persist_setup(vp3d_stream* st, int dtype) {
     p.queue = kQueue;
     p.poses = st->out_pose;
     p.frames_seen = st->frames_seen;
-    st->hand_bytes = 16 + (size_t)(2 * nb + 1) * 2 * C * 8;
+    st->hand_bytes = (size_t)(2 * nb + 1) * 2 * C * 8;
     if (hipMalloc(&st->hand, st->hand_bytes) != hipSuccess) return false;
     if (hipMalloc(&st->pstate, (size_t)p.G * p.state_floats * 4) != hipSuccess) {
         hipFree(st->hand);
@@ -801,8 +878,8 @@ bool stream_persist_setup(vp3d_stream* st, int dtype) {
         return false;
     }
     hipMemset(st->pstate, 0, (size_t)p.G * p.state_floats * 4);
-    p.err = (unsigned*)st->hand;
-    p.gran = (unsigned long long*)((char*)st->hand + 16);
+    p.fault = StreamFault{(unsigned*)(st->frames_seen + 3), st->err_host_dev, st->spin_ticks};
+    p.gran = (unsigned long long*)st->hand;
     p.state = st->pstate;
     return true;
 }
@@ -882,7 +959,7 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     p.poses = st->out_pose;
     p.frames_seen = st->frames_seen;
     p.arrivals = (unsigned*)(st->frames_seen + 2);
-    p.err = (unsigned*)(st->frames_seen + 3);
+    p.fault = StreamFault{(unsigned*)(st->frames_seen + 3), st->err_host_dev, st->spin_ticks};
     p.gran = st->pipe_gran;
     p.state = st->pipe_state;
     return true;
@@ -1005,6 +1082,13 @@ int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out) {
         q.done_counter = (unsigned*)(st->frames_seen + 1);
         st->steps.push_back(q);
     }
+    if (const char* e = getenv("VP3D_STREAM_SPIN_TICKS")) st->spin_ticks = strtoull(e, nullptr, 10);
+    if (hipHostMalloc(&st->err_host, 4, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&st->err_host_dev, st->err_host, 0) != hipSuccess) {
+        hipHostFree(st->err_host);
+        return cleanup(fail(VP3D_ERR_OOM, "stream fault word"));
+    }
+    *(volatile unsigned*)st->err_host = 0u;
     st->pipe = stream_pipe_setup(st, dtype);
     if (!st->pipe) st->persist = stream_persist_setup(st, dtype);
     hipDeviceSynchronize();  // setup memsets (legacy stream) before any launch on another stream
@@ -1020,14 +1104,18 @@ int vp3d_stream_status(vp3d_stream* st) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     if (!st->persist && !st->pipe) return VP3D_OK;
     unsigned err = 0;
-    HIP_TRY(hipMemcpy(&err, st->pipe ? (void*)(st->frames_seen + 3) : st->hand, 4, hipMemcpyDeviceToHost));
-    if (err) return fail(VP3D_ERR_STATE, "persistent stream step timed out waiting for another CU");
+    HIP_TRY(hipMemcpy(&err, (void*)(st->frames_seen + 3), 4, hipMemcpyDeviceToHost));
+    if (err) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
     return VP3D_OK;
 }
 
 int vp3d_stream_reset(vp3d_stream* st, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    // position, arrival counter and the sticky timeout word; the host mirror is cleared
+    // once no launch of this stream can still set it
     HIP_TRY(hipMemsetAsync(st->frames_seen, 0, 16, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    *(volatile unsigned*)st->err_host = 0u;
     // pipelined form: granule tags restart at frame 1
     if (st->pipe) HIP_TRY(hipMemsetAsync(st->pipe_gran, 0, st->pipe_gran_bytes, (hipStream_t)stream));
     st->host_t = 0;
@@ -1044,6 +1132,7 @@ int vp3d_stream_io(vp3d_stream* st, float** in_frames, float** out_poses, int* q
 
 int vp3d_stream_step(vp3d_stream* st, const float* frame, float* pose, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
     hipStream_t s = (hipStream_t)stream;
     const int slot = (int)(st->host_t % kQueue);
     const int cin = st->h->layers[0].cin, cout = st->h->layers.back().cout;
@@ -1094,6 +1183,7 @@ int vp3d_stream_graph_capture(vp3d_stream* st, void* stream, int steps) {
 
 int vp3d_stream_graph_launch(vp3d_stream* st, void* stream) {
     if (!st || !st->exec) return fail(VP3D_ERR_STATE, "no captured graph");
+    if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
     HIP_TRY(hipGraphLaunch(st->exec, (hipStream_t)stream));
     st->host_t += st->graph_steps;
     return VP3D_OK;
@@ -1112,6 +1202,7 @@ int vp3d_stream_destroy(vp3d_stream* st) {
     hipFree(st->pstate);
     hipFree(st->pipe_gran);
     hipFree(st->pipe_state);
+    hipHostFree(st->err_host);
     delete st;
     return VP3D_OK;
 }

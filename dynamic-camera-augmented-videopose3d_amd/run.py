@@ -46,14 +46,51 @@ def synthetic_dataset(args, normalize=None):
             for s, acts in raw.items()}
 
 
-def load_data(args):
-    """The split run.py evaluates / trains on: synthetic or the reference's .npz files."""
+def load_data(args, stride=None):
+    """The split run.py evaluates / trains on: synthetic or the reference's .npz files,
+    every `stride`-th frame (default --downsample; 1 = undecimated)."""
     from vp3d_amd.datasets import downsample, load_dataset
     if args.dataset == "synthetic":
         data = synthetic_dataset(args)
     else:
         _, data, _ = load_dataset(args.dataset, args.data_dir, args.keypoints)
-    return downsample(data, args.downsample)
+    return downsample(data, args.downsample if stride is None else stride)
+
+
+def deterministic_random(min_value, max_value, data):
+    """Hash-seeded integer in [min_value, max_value) (reference common/utils.py:44-47)."""
+    import hashlib
+    digest = hashlib.sha256(data.encode()).digest()
+    raw_value = int.from_bytes(digest[:4], byteorder='little', signed=False)
+    return int(raw_value / (2 ** 32 - 1) * (max_value - min_value)) + min_value
+
+
+def subset_views(cams, p3d, p2d, subset=1.0, stride=1):
+    """The tail of the reference's fetch (run.py:168-180) on undecimated views: with
+    subset < 1 every view keeps round(len // stride * subset) * stride frames starting at
+    deterministic_random(0, len - n + 1, str(len)), every stride-th of them; otherwise
+    every stride-th frame (--downsample).  The per-frame camera extrinsics are sliced with
+    the poses -- the reference leaves camera params whole, which only its static-camera
+    datasets tolerate; here K.E stays aligned with the frames it belongs to."""
+    if subset >= 1 and stride <= 1:
+        return cams, p3d, p2d
+    cams, p3d, p2d = list(cams), list(p3d), list(p2d)
+    for i in range(len(p2d)):
+        if subset < 1:
+            L = len(p2d[i])
+            n = int(round(L // stride * subset) * stride)
+            start = deterministic_random(0, L - n + 1, str(L))
+            sl = slice(start, start + n, stride)
+        else:
+            sl = slice(None, None, stride)
+        p2d[i] = p2d[i][sl]
+        if p3d is not None:
+            p3d[i] = p3d[i][sl]
+        if cams is not None and "extrinsics" in cams[i]:
+            c = dict(cams[i])
+            c["extrinsics"] = c["extrinsics"][sl]
+            cams[i] = c
+    return cams, p3d, p2d
 
 
 def joint_counts(data):
@@ -229,8 +266,12 @@ def train_main(args, data):
     model_pos = build_model(args, j2, announce=False, J_out=j3).cuda()
     pad = (model_pos.receptive_field() - 1) // 2
     causal_shift = pad if args.causal else 0
-    cams_tr, p3d_tr, p2d_tr = fetch(data, subjects_train, action_filter)
-    cams_te, p3d_te, p2d_te = fetch(data, subjects_test, action_filter)
+    # `data` is undecimated here: the training views get the reference fetch's --subset /
+    # --downsample rule (run.py:168-180, fetch(..., subset=args.subset) at :656), the test
+    # views --downsample only (run.py:657)
+    cams_tr, p3d_tr, p2d_tr = subset_views(*fetch(data, subjects_train, action_filter), subset=args.subset,
+                                           stride=args.downsample)
+    cams_te, p3d_te, p2d_te = subset_views(*fetch(data, subjects_test, action_filter), stride=args.downsample)
     resume = None
     if args.resume:
         path = os.path.join(args.checkpoint, args.resume)
@@ -266,9 +307,11 @@ def main(argv=None):
         raise SystemExit(f"--use-model {args.model_name}: only the FCN lifter runs on this path")
     if not torch.cuda.is_available():
         raise SystemExit("run.py evaluates on the MI355X (no CPU fallback)")
-    data = load_data(args)
     if not args.evaluate:
-        return train_main(args, data)
+        return train_main(args, load_data(args, stride=1))
+    if args.subset < 1:
+        raise SystemExit("--subset applies to training (run.py:656); evaluation reads whole sequences")
+    data = load_data(args)
     subjects = list(data.keys()) if args.subjects_test in (None, "*") else args.subjects_test.split(",")
     j2, j3 = joint_counts(data)
     model = build_model(args, j2, J_out=j3).cuda().eval()

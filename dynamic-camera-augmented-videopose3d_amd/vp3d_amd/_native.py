@@ -31,9 +31,11 @@ VARIANT_STRIDED_1F = 1
 DTYPE_F32 = 0
 DTYPE_BF16 = 1
 DTYPE_F16 = 2
+DTYPE_F16X3 = 3
 DTYPES = {"fp32": DTYPE_F32, "float32": DTYPE_F32, "f32": DTYPE_F32,
           "bf16": DTYPE_BF16, "bfloat16": DTYPE_BF16,
-          "fp16": DTYPE_F16, "float16": DTYPE_F16, "f16": DTYPE_F16}
+          "fp16": DTYPE_F16, "float16": DTYPE_F16, "f16": DTYPE_F16,
+          "f16x3": DTYPE_F16X3}
 
 MAX_BLOCKS = 8
 
@@ -197,7 +199,8 @@ def _check_provenance(lib) -> None:
     got = lib.vp3d_build_hash().decode()
     if got != want:
         raise ImportError(
-            f"vp3d: {_LIB_PATH} was built from other sources (library {got[:16]}, tree {want[:16]}); "
+            f"vp3d: {_LIB_PATH} was built from other sources or for another target (library {got[:16]}, "
+            f"tree {want[:16]} for arch {_build.ARCH}, VP3D_OFFLOAD_ARCH); "
             "rebuild with `python __graft_entry__.py build`")
 
 

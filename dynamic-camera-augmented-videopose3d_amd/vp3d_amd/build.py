@@ -1,9 +1,10 @@
 """In-tree build of libvp3d.so (the C-ABI of include/vp3d.h) for gfx950.
 
-Plain `hipcc` per translation unit, then one shared-library link.  Objects are
-rebuilt only when a source or header is newer than the object, so repeated
-builds are cheap.  The library lands next to this file so that it travels to
-the GPU box with the repository snapshot.
+Plain `hipcc` per translation unit, then one shared-library link.  An object is
+rebuilt only when its own source, or the shared configuration (target arch, flags,
+any header, this recipe), changed -- by content hash, recorded beside the object --
+so editing one kernel recompiles one file.  The library lands next to this file so
+that it travels to the GPU box with the repository snapshot.
 """
 from __future__ import annotations
 
@@ -22,8 +23,6 @@ LIB_PATH = os.path.join(PKG_DIR, "libvp3d.so")
 SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_8p.hip", "conv_gemm_q64.hip", "expand_gemm.hip", "preprocess.hip",
            "metrics.hip", "stream_step.hip", "stream_persist.hip", "stream_pipe.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp",
            "vp3d_seq.cpp"]
-HEADERS = [os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "gemm_common.h"), os.path.join(CSRC, "host.h"),
-           os.path.join(INCLUDE, "vp3d.h")]
 ARCH = os.environ.get("VP3D_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -70,11 +69,32 @@ def embedded_hash(path: str = LIB_PATH):
     return m.group(1).decode() if m else None
 
 
-def _newer(src_paths, dst):
-    if not os.path.exists(dst):
+def _config_hash() -> str:
+    """Hash of what every object depends on besides its own source: arch, flags, the
+    headers under csrc/ and include/, and this recipe."""
+    import hashlib
+    h = hashlib.sha256(("arch=" + ARCH + ";flags=" + " ".join(COMMON_FLAGS)).encode())
+    for f in _hashed_files()[len(SOURCES):]:
+        h.update(os.path.relpath(f, REPO).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _tu_hash(config: str, src: str) -> str:
+    import hashlib
+    h = hashlib.sha256(config.encode())
+    with open(src, "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()
+
+
+def _stale(obj: str, tu: str) -> bool:
+    try:
+        with open(obj + ".sha") as f:
+            return f.read().strip() != tu or not os.path.exists(obj)
+    except OSError:
         return True
-    t = os.path.getmtime(dst)
-    return any(os.path.getmtime(p) > t for p in src_paths)
 
 
 def _run(cmd):
@@ -91,8 +111,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
 
     os.makedirs(BUILD_DIR, exist_ok=True)
     want = source_hash()
-    if embedded_hash() != want:
-        force = True  # built from other sources (or by another recipe): rebuild everything
+    config = _config_hash()
     objs, todo = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
@@ -100,22 +119,28 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
             continue
         obj = os.path.join(BUILD_DIR, s + ".o")
         objs.append(obj)
-        if force or _newer([src] + HEADERS, obj):
+        tu = _tu_hash(config, src)
+        if force or _stale(obj, tu):
             if s.endswith(".hip"):
                 cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}"] + COMMON_FLAGS + ["-c", src, "-o", obj]
             else:
                 cmd = [HIPCC] + COMMON_FLAGS + ["-c", src, "-o", obj]
-            todo.append(cmd)
+            todo.append((cmd, obj, tu))
     if todo:
         jobs = jobs or max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
-        for cmd in todo:
+        for cmd, obj, _ in todo:
             if verbose:
                 print("$", " ".join(cmd), flush=True)
+            if os.path.exists(obj + ".sha"):
+                os.remove(obj + ".sha")
         with ThreadPoolExecutor(jobs) as ex:
-            for out in ex.map(_run, todo):
+            for out in ex.map(_run, [t[0] for t in todo]):
                 if verbose and out.strip():
                     print(out)
-    if force or _newer(objs, LIB_PATH):
+        for _, obj, tu in todo:
+            with open(obj + ".sha", "w") as f:
+                f.write(tu + "\n")
+    if force or todo or embedded_hash() != want:
         # provenance: one generated translation unit carrying the source hash
         info_src = os.path.join(BUILD_DIR, "build_info.cpp")
         info_obj = info_src + ".o"

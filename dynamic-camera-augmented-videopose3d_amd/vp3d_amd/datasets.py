@@ -138,7 +138,10 @@ def load_dataset(name: str, data_dir: str, keypoints: str = "gt", device=None):
 
 
 def downsample(data: dict, stride: int) -> dict:
-    """--downsample (run.py:903-910): every stride-th frame of every view."""
+    """--downsample (run.py:903-910): every stride-th frame of every view.  Divergence,
+    on purpose: each camera record's per-frame extrinsics are decimated with the poses
+    (the reference slices only the 2D / 3D poses, run.py:175-180, leaving its moving-camera
+    K.E tables one frame per ORIGINAL frame, misaligned with the decimated poses)."""
     if stride <= 1:
         return data
     out = {}

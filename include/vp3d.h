@@ -49,6 +49,12 @@ extern "C" {
 #define VP3D_DTYPE_F32 0  /* exact f32 MFMA (v_mfma_f32_16x16x4_f32), the parity path */
 #define VP3D_DTYPE_BF16 1 /* bf16 operands, f32 accumulate (v_mfma_f32_16x16x32_bf16) */
 #define VP3D_DTYPE_F16 2  /* f16 operands, f32 accumulate (v_mfma_f32_16x16x32_f16)   */
+/* split fp16: every f32 operand carried as hi + lo f16 halves (weights pre-scaled by a
+ * per-layer power of two), each conv the three products hi.hi + hi.lo + lo.hi on
+ * v_mfma_f32_16x16x32_f16 with f32 accumulation -- fp32-level results (the parity gate)
+ * at the 16-bit MFMA rate; eval forward only (vp3d_forward / vp3d_forward_windows),
+ * channels % 64 == 0 and <= 1024; the shrink runs the exact f32 GEMM */
+#define VP3D_DTYPE_F16X3 3
 
 /* Model configuration: the constructor arguments of TemporalModel /
  * TemporalModelOptimized1f (TemporalModel.py:85-86, :152-153). */

@@ -59,3 +59,47 @@ def test_checkpoint_loader_admits_run_checkpoint_only(tmp_path):
     torch.save({"model_pos": sd, "x": Evil()}, bad)
     with pytest.raises(RuntimeError, match="trust-checkpoint"):
         load_checkpoint(bad)
+
+
+def test_subset_views_matches_reference_fetch():
+    """--subset / --downsample on the training views (reference run.py:168-180): the trimmed
+    lengths and start frames.  The starts are the reference's own deterministic_random
+    (common/utils.py:44-47) values, pinned by importing it in the build container."""
+    import run
+    want_start = {1000: 411, 2048: 1008, 517: 345, 300: 22}  # deterministic_random(0, L - n + 1, str(L))
+    for L, n in ((1000, 100), (2048, 204), (517, 50), (300, 30)):
+        assert run.deterministic_random(0, L - n + 1, str(L)) == want_start[L]
+    lens = [1000, 2048, 517]
+    p2d = [np.arange(L * 2, dtype=np.float32).reshape(L, 1, 2) for L in lens]
+    p3d = [np.arange(L * 3, dtype=np.float32).reshape(L, 1, 3) for L in lens]
+    cams = [{"intrinsics": {}, "extrinsics": np.arange(L * 12, dtype=np.float64).reshape(L, 3, 4)} for L in lens]
+    for subset, stride in ((0.1, 1), (0.1, 2), (1.0, 3), (0.5, 3)):
+        c2, q3, q2 = run.subset_views(cams, p3d, p2d, subset=subset, stride=stride)
+        for i, L in enumerate(lens):
+            if subset < 1:
+                n = int(round(L // stride * subset) * stride)
+                start = run.deterministic_random(0, L - n + 1, str(L))
+                idx = np.arange(start, start + n, stride)
+            else:
+                idx = np.arange(0, L, stride)
+            assert q2[i].shape[0] == q3[i].shape[0] == c2[i]["extrinsics"].shape[0] == len(idx)
+            np.testing.assert_array_equal(q2[i][:, 0, 0], 2 * idx)
+            np.testing.assert_array_equal(q3[i][:, 0, 0], 3 * idx)
+            np.testing.assert_array_equal(c2[i]["extrinsics"][:, 0, 0], 12 * idx)
+    # the inputs are untouched
+    assert p2d[0].shape[0] == 1000 and cams[0]["extrinsics"].shape[0] == 1000
+    c2, q3, q2 = run.subset_views(cams, p3d, p2d)  # subset 1, stride 1: the views as they are
+    assert q2 is p2d and q3 is p3d and c2 is cams
+
+
+def test_downsample_slices_extrinsics_with_poses():
+    """--downsample 2 on a CMU-style split: 2D, 3D and per-frame extrinsics keep equal
+    lengths (the documented divergence from the reference, which leaves K.E undecimated)."""
+    from vp3d_amd.datasets import downsample
+    data = {"01": {"walk_0": {"positions_3d": [np.zeros((301, 17, 3), np.float32)],
+                              "keypoints": [np.zeros((301, 17, 2), np.float32)],
+                              "cameras": [{"intrinsics": {}, "extrinsics": np.zeros((301, 3, 4))}]}}}
+    d = downsample(data, 2)["01"]["walk_0"]
+    assert d["positions_3d"][0].shape[0] == d["keypoints"][0].shape[0] == 151
+    assert d["cameras"][0]["extrinsics"].shape[0] == 151
+    assert downsample(data, 1) is data

@@ -39,11 +39,13 @@ def build(meta, g):
     return m.eval().cuda()
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
 @pytest.mark.parametrize("name", CASES)
-def test_native_fp32_matches_reference(name):
+def test_native_fp32_matches_reference(name, dtype):
+    """fp32 and the split-fp16 path (f16x3) under the north-star gate."""
     g = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
     meta = json.loads(str(g["meta"]))
-    m = build(meta, g)
+    m = build(meta, g).set_compute_dtype(dtype)
     with torch.no_grad():
         y = m(torch.from_numpy(g["x"]).cuda()).cpu().numpy()
     ref = g["y"]
@@ -51,7 +53,7 @@ def test_native_fp32_matches_reference(name):
     gt = synth.gt_poses(3, name, ref.shape[0] * ref.shape[1], 17).reshape(ref.shape)
     d = abs(mpjpe_np(y, gt) - mpjpe_np(ref, gt))
     err = float(np.abs(y - ref).max())
-    print(f"{name}: max|d|={err:.3e} m dMPJPE={d * 1e3:.3e} mm")
+    print(f"{name} {dtype}: max|d|={err:.3e} m dMPJPE={d * 1e3:.3e} mm")
     assert err <= 1e-5
     assert d * 1e3 <= 1e-4
 

@@ -4,6 +4,8 @@ Tolerances (stated per the north star, SURVEY.md §7 "Hard parts"):
   fp32  : |MPJPE(native, GT) - MPJPE(oracle, GT)| <= 1e-7 m (= 1e-4 mm) and every
           coordinate within 1e-5 m of the oracle (the reference's own fp32
           deviation from exact arithmetic is ~2e-7 m on these weights).
+  f16x3 : the split-fp16 path (every f32 operand as hi + lo f16 halves, three 16-bit MFMA
+          products per conv) is held to the fp32 gates above.
   bf16 / fp16 : measured separately; gates about 3x the largest error measured on
           MI355X over these cases (bf16 operands carry 8 mantissa bits, fp16 11).
 """
@@ -45,7 +47,7 @@ def _check(y, ref, gt, dtype):
     d_mpjpe = abs(mpjpe_np(y, gt) - mpjpe_np(ref, gt))
     print(f"{dtype}: max|d|={err:.3e} m  dMPJPE={d_mpjpe * 1e3:.3e} mm")
     assert np.isfinite(y).all()
-    if dtype == "fp32":
+    if dtype in ("fp32", "f16x3"):
         assert err <= FP32_COORD_TOL, err
         assert d_mpjpe <= FP32_MPJPE_TOL, d_mpjpe
     else:
@@ -53,10 +55,11 @@ def _check(y, ref, gt, dtype):
         assert d_mpjpe <= H16_TOL[dtype][1], d_mpjpe
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
 @pytest.mark.parametrize("causal", [False, True])
-def test_opt1f_243_fp32(causal):
-    y, ref, gt = _run(True, 64, 243, causal=causal)
-    _check(y, ref, gt, "fp32")
+def test_opt1f_243_fp32(causal, dtype):
+    y, ref, gt = _run(True, 64, 243, causal=causal, dtype=dtype)
+    _check(y, ref, gt, dtype)
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
@@ -65,7 +68,7 @@ def test_opt1f_243_h16(dtype):
     _check(y, ref, gt, dtype)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "f16x3"])
 def test_opt1f_243_h16_large_batch(dtype):
     # B = 2050 windows: the block-1/2 layers (M = 55,350 / 18,450 rows, the last
     # 256-row tile partial) run on the 256x256 whole-line kernel (q64) and the expand
@@ -86,7 +89,7 @@ def _config4_ref():
     return _CONFIG4["model"], _CONFIG4["xs"], _CONFIG4["ref"]
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32", "f16x3"])
 def test_config4_b65536(dtype):
     """Config 4's whole global batch on one GPU: B = 65,536 windows (243 frames, 1024 ch),
     the shape the headline bench times.  The block-1 outputs are 3.6 GB in bf16 (past 2^31
@@ -108,9 +111,9 @@ def test_config4_b65536(dtype):
     gt = synth.gt_poses(3, "gt", 64 * ref.shape[1], 17).reshape(ref.shape)
     for r in (0, 1, reps // 2, reps - 2, reps - 1):
         _check(y[r], ref, gt, dtype)
-    tol = FP32_COORD_TOL if dtype == "fp32" else H16_TOL[dtype][0]
+    tol = FP32_COORD_TOL if dtype in ("fp32", "f16x3") else H16_TOL[dtype][0]
     assert np.abs(y - ref[None]).max() <= tol
-    if dtype == "fp32":
+    if dtype in ("fp32", "f16x3"):
         # tiles of identical windows: the same rows of every tile give the same bits
         assert np.array_equal(y[0], y[reps - 1])
 
@@ -137,16 +140,18 @@ def test_dilated_long_seq_bf16():
     _check(y, ref, gt, "bf16")
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
 @pytest.mark.parametrize("causal", [False, True])
-def test_dilated_seq_243_fp32(causal):
-    y, ref, gt = _run(False, 1, 600, causal=causal)
-    _check(y, ref, gt, "fp32")
+def test_dilated_seq_243_fp32(causal, dtype):
+    y, ref, gt = _run(False, 1, 600, causal=causal, dtype=dtype)
+    _check(y, ref, gt, dtype)
 
 
-def test_dilated_batch_ragged_fp32():
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
+def test_dilated_batch_ragged_fp32(dtype):
     # B=3 sequences, lengths give M not a multiple of the 128-row tile
-    y, ref, gt = _run(False, 3, 300, fw=(3, 3, 3), channels=256)
-    _check(y, ref, gt, "fp32")
+    y, ref, gt = _run(False, 3, 300, fw=(3, 3, 3), channels=256, dtype=dtype)
+    _check(y, ref, gt, dtype)
 
 
 def test_dilated_27_bf16():
@@ -154,20 +159,32 @@ def test_dilated_27_bf16():
     _check(y, ref, gt, "bf16")
 
 
-def test_dense_ablation_fp32():
-    y, ref, gt = _run(False, 1, 120, fw=(3, 3, 3), channels=128, dense=True)
-    _check(y, ref, gt, "fp32")
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
+def test_dense_ablation_fp32(dtype):
+    y, ref, gt = _run(False, 1, 120, fw=(3, 3, 3), channels=128, dense=True, dtype=dtype)
+    _check(y, ref, gt, dtype)
 
 
-def test_small_channels_odd_joints():
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
+def test_small_channels_odd_joints(dtype):
     # trajectory-conditioned shape: 23 input "joints" (17 kp + 6 camera pairs), C=64
-    y, ref, gt = _run(True, 5, 27, fw=(3, 3, 3), channels=64, jin=23)
-    _check(y, ref, gt, "fp32")
+    y, ref, gt = _run(True, 5, 27, fw=(3, 3, 3), channels=64, jin=23, dtype=dtype)
+    _check(y, ref, gt, dtype)
 
 
-def test_width5_blocks():
-    y, ref, gt = _run(False, 2, 200, fw=(3, 5, 3), channels=128)
-    _check(y, ref, gt, "fp32")
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
+def test_width5_blocks(dtype):
+    y, ref, gt = _run(False, 2, 200, fw=(3, 5, 3), channels=128, dtype=dtype)
+    _check(y, ref, gt, dtype)
+
+
+def test_f16x3_unsupported_channels():
+    """The split path needs channels % 64 == 0 (<= 1024): other widths raise, never a
+    silent fallback."""
+    m, _ = make_model(True, fw=(3, 3), channels=96)
+    m.cuda().set_compute_dtype("f16x3")
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(2, 9, 17, 2, device="cuda"))
 
 
 def test_weights_reload_and_equivalence():

@@ -69,7 +69,7 @@ def _worker(rank, world, port, outdir, dtype):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype", ["bf16"])
+@pytest.mark.parametrize("dtype", ["bf16", "f16x3"])
 def test_config4_two_ranks_bit_equal(tmp_path, dtype):
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), dtype), nprocs=world, join=True)

@@ -112,3 +112,36 @@ def test_stream_rejects_noncausal():
     m.cuda()
     with pytest.raises(RuntimeError):
         CausalStream(m.native_lifter(), "fp16")
+
+
+@pytest.mark.parametrize("mode", ["pipe", "persist"])
+def test_stream_timeout_is_sticky(mode, monkeypatch):
+    """Fault injection: VP3D_STREAM_SPIN_TICKS=0 makes the first unanswered poll of a
+    persistent step time out.  The timeout word is sticky: check() raises, later step()s
+    and graph replays are refused by the host (no synchronisation needed) and the device
+    launches become no-ops, so the stream position never drifts; reset() clears it."""
+    monkeypatch.setenv("VP3D_STREAM_MODE", mode)
+    monkeypatch.setenv("VP3D_STREAM_SPIN_TICKS", "0")
+    m, _ = make_model(False, (3, 3, 3), causal=True, channels=256)
+    m.cuda()
+    st = CausalStream(m.native_lifter(), "fp16")
+    assert st.mode == mode
+    xs = torch.from_numpy(synth.normalized_windows(17, "stream_fault", 1, 8)[0]).cuda()
+    failed_at = None
+    for t in range(8):
+        try:
+            st.step(xs[t])
+        except RuntimeError:
+            failed_at = t
+            break
+        torch.cuda.synchronize()
+    assert failed_at is not None, "no step timed out with a zero spin budget"
+    with pytest.raises(RuntimeError, match="timed out"):
+        st.check()
+    with pytest.raises(RuntimeError, match="timed out"):
+        st.step(xs[0])
+    seen = st.frames_seen()
+    assert 0 <= seen < failed_at
+    st.reset()
+    st.check()
+    assert st.frames_seen() == 0

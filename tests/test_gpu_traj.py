@@ -98,8 +98,10 @@ def test_traj_dolly_windows_h16(dtype):
     assert err <= ce and d <= me, (err, d)
 
 
-def test_traj_dolly_windows_fp32():
-    """fp32 on the same windows meets the north-star gate (|dMPJPE| <= 1e-4 mm)."""
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
+def test_traj_dolly_windows_fp32(dtype):
+    """fp32 and the split-fp16 path on the same windows meet the north-star gate
+    (|dMPJPE| <= 1e-4 mm); f16x3 through the split pack kernel's gather + concat."""
     from vp3d_amd.pipeline import SyntheticWindowPool
     model, sd = _model()
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -108,9 +110,9 @@ def test_traj_dolly_windows_fp32():
     pairs = torch.from_numpy(pool.global_pairs(B)).to(dev)
     lifter = model.native_lifter(dev)
     with torch.no_grad():
-        y = lifter.forward_windows(pool.seqs, pairs, 243, 121, concat_cams=True, dtype="fp32").cpu().numpy()
+        y = lifter.forward_windows(pool.seqs, pairs, 243, 121, concat_cams=True, dtype=dtype).cpu().numpy()
         x = pool.seqs.gather(pairs, 243, 121, "2d", concat_cams=True).view(B, 243, 23, 2).cpu()
     ref = lifter_forward(sd, x, [3, 3, 3, 3, 3], strided=True).numpy()
     gt = synth.gt_poses(3, "dolly_gt", B, 17).reshape(ref.shape)
-    err, d = _report(y, ref, gt, "dolly fp32")
+    err, d = _report(y, ref, gt, f"dolly {dtype}")
     assert err <= 2e-5 and d <= 1e-7, (err, d)

@@ -34,16 +34,19 @@ from bf16_error_study import keys_shapes  # noqa: E402
 h16 = lambda t: t.to(torch.float16).float()  # noqa: E731
 
 
+LO_SCALE = 1.0  # 2^11: lo carried scaled (kernel variant A); 1: unscaled lo (interleaved variant)
+
+
 def split(x):
     hi = h16(x)
-    return hi, h16((x - hi) * 2048.0)
+    return hi, h16((x - hi) * LO_SCALE)
 
 
 def wsplit(W):
     e = 14 - int(np.floor(np.log2(float(W.abs().max()))))
     Ws = W * (2.0 ** e)
     Wh = h16(Ws)
-    return Wh, h16(Wh * 2.0 ** -11), h16(Ws - Wh), 2.0 ** -e
+    return Wh, h16(Wh / LO_SCALE), h16(Ws - Wh), 2.0 ** -e
 
 
 def emulate(sd, x, fw, eps=1e-5):
@@ -67,7 +70,7 @@ def emulate(sd, x, fw, eps=1e-5):
         return F.relu(acc * (sc * inv_s)[:, None] + sh[:, None])
 
     def join(p):
-        return p[0] + p[1] * 2.0 ** -11
+        return p[0] + p[1] / LO_SCALE
 
     B, T = x.shape[:2]
     h = torch.from_numpy(x).reshape(B, T, -1).permute(0, 2, 1).contiguous()
@@ -89,7 +92,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--traj", action="store_true")
+    ap.add_argument("--lo-scale", type=float, default=1.0)
     a = ap.parse_args()
+    global LO_SCALE
+    LO_SCALE = a.lo_scale
     fw = [3, 3, 3, 3, 3]
     jin = 23 if a.traj else 17
     sd = synth.lifter_state_dict(keys_shapes(jin, fw, 1024), seed=0)
