@@ -186,6 +186,7 @@ hipError_t launch_stream_pipe(const StreamPipeParams& p, Act wtype, int lds_byte
 // preprocess kernels (preprocess.hip)
 hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, float* out,
                                    bool inverse, hipStream_t s);
+hipError_t launch_normalize_screen_f64(const double* x, int64_t n, double w, double hw, float* out, hipStream_t s);
 hipError_t launch_camera_matrices(const float* intr, const int32_t* frame_seq, const double* extr,
                                   int64_t n_frames, float* out, hipStream_t s);
 hipError_t launch_world_to_camera(const float* X, int64_t n, const float q[4], const float t[3],

@@ -56,6 +56,19 @@ __global__ void normalize_screen_kernel(const float* __restrict__ x, int64_t n, 
     }
 }
 
+// float64 keypoints (3DPW): X / w * 2 - [1, hw] entirely in float64, rounded once
+__global__ void normalize_screen_f64_kernel(const double* __restrict__ x, int64_t n, double w, double hw,
+                                            float* __restrict__ out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double2 v = reinterpret_cast<const double2*>(x)[i];
+        float2 r;
+        r.x = (float)__dsub_rn(__dmul_rn(__ddiv_rn(v.x, w), 2.0), 1.0);
+        r.y = (float)__dsub_rn(__dmul_rn(__ddiv_rn(v.y, w), 2.0), hw);
+        reinterpret_cast<float2*>(out)[i] = r;
+    }
+}
+
 // K (float32, from the sequence's intrinsics) @ E_t (float64) in float64,
 // rounded once to float32 when run.py casts the batch (`astype('float32')`).
 // K = [[fx,0,cx],[0,fy,cy],[0,0,1]] so each entry has at most two non-zero
@@ -221,6 +234,13 @@ hipError_t launch_normalize_screen(const float* x, int64_t n, int w, int h, floa
     const double hw = (double)h / (double)w;
     hipLaunchKernelGGL(normalize_screen_kernel, grid_for(n, 4), dim3(kThreads), 0, s, x, n,
                        (float)w, hw, out, inverse ? 1 : 0, 0.f);
+    return hipGetLastError();
+}
+
+hipError_t launch_normalize_screen_f64(const double* x, int64_t n, double w, double hw, float* out,
+                                       hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(normalize_screen_f64_kernel, grid_for(n, 4), dim3(kThreads), 0, s, x, n, w, hw, out);
     return hipGetLastError();
 }
 

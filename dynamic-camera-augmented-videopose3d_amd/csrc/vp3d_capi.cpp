@@ -1217,6 +1217,13 @@ int vp3d_normalize_screen(const float* x, int64_t n_points, int32_t w, int32_t h
     return VP3D_OK;
 }
 
+int vp3d_normalize_screen_f64(const double* x, int64_t n_points, double w, double hw, float* out, void* stream) {
+    if (!x || !out) return fail(VP3D_ERR_ARG, "x / out is NULL");
+    if (!(w > 0.0)) return fail(VP3D_ERR_ARG, "w must be positive");
+    HIP_TRY(launch_normalize_screen_f64(x, n_points, w, hw, out, (hipStream_t)stream));
+    return VP3D_OK;
+}
+
 int vp3d_image_coordinates(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,
                            void* stream) {
     if (n_points < 0 || (n_points > 0 && (!x || !out))) return fail(VP3D_ERR_ARG, "bad pointer");

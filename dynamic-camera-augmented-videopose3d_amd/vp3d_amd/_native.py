@@ -45,7 +45,7 @@ EXPORTS = [
     "vp3d_receptive_field", "vp3d_total_causal_shift", "vp3d_out_frames",
     "vp3d_reserve", "vp3d_forward", "vp3d_forward_windows", "vp3d_profile_enable", "vp3d_layer_count",
     "vp3d_profile_read", "vp3d_profile_reset", "vp3d_profile_layers", "vp3d_normalize_screen",
-    "vp3d_image_coordinates", "vp3d_camera_matrices", "vp3d_world_to_camera",
+    "vp3d_normalize_screen_f64", "vp3d_image_coordinates", "vp3d_camera_matrices", "vp3d_world_to_camera",
     "vp3d_gather_windows", "vp3d_mpjpe_accumulate", "vp3d_pose_metrics", "vp3d_project_to_2d", "vp3d_last_error", "vp3d_abi_version",
     "vp3d_build_hash",
     "vp3d_stream_create", "vp3d_stream_reset", "vp3d_stream_io", "vp3d_stream_step",
@@ -121,6 +121,7 @@ _SIGNATURES = {
     "vp3d_profile_reset": (_int, [_vp]),
     "vp3d_profile_layers": (_int, [_vp, ctypes.c_uint64]),
     "vp3d_normalize_screen": (_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
+    "vp3d_normalize_screen_f64": (_int, [_vp, _i64, ctypes.c_double, ctypes.c_double, _vp, _vp]),
     "vp3d_image_coordinates": (_int, [_vp, _i64, _i32, _i32, _vp, _vp]),
     "vp3d_camera_matrices": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "vp3d_world_to_camera": (_int, [_vp, _i64, _vp, _vp, _vp, _vp]),

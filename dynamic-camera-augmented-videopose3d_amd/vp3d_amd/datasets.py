@@ -10,10 +10,14 @@ run.py's form:
                         "cameras":      [camera record per view]}}}
 
 Per dataset, as run.py:65-124 prepares it:
-  CMU / CMU_3DPW  positions -= positions[:, :1] (quirk Q3: the root joint becomes 0);
+  CMU / CMU_3DPW / 3DPW
+                  positions -= positions[:, :1] (quirk Q3: the root joint becomes 0);
                   one view per action; keypoints normalised with the CMU resolution;
                   the camera record is the dataset's own (normalised K, per-frame E,
-                  camera-motion statistics).
+                  camera-motion statistics; 3DPW: its per-sequence intrinsics and the
+                  motion means of ThreeDPWDataset.py:60-85).  3DPW keypoints are float64
+                  with a float32 resolution 2 c_x, 2 c_y: normalised in float64 and
+                  rounded once (vp3d_normalize_screen_f64).
   h36m            one view per calibrated camera: world_to_camera(positions, R, t)
                   (vp3d_world_to_camera, bit-exact with the reference's torch-CPU qrot),
                   then joints 1.. made root-relative, the root keeping the trajectory;
@@ -34,14 +38,22 @@ import numpy as np
 import torch
 
 MOTION_KEYS = ("cam_velocity", "cam_acceleration", "cam_angular_velocity", "cam_angular_acceleration")
-DATASETS_3D = ("h36m", "CMU", "CMU_3DPW")
+DATASETS_3D = ("h36m", "CMU", "CMU_3DPW", "3DPW")
+MOVING_CAMERA = ("CMU", "CMU_3DPW", "3DPW")  # one view per action, per-frame extrinsics
 
 
-def _normalize(kps: np.ndarray, w: int, h: int, device) -> np.ndarray:
-    from .pipeline import normalize_screen
-    x = torch.from_numpy(np.ascontiguousarray(kps[..., :2], dtype=np.float32)).to(device)
+def _normalize(kps: np.ndarray, w, h, device) -> np.ndarray:
+    from .pipeline import normalize_screen, normalize_screen_f64
     out = np.array(kps, dtype=np.float32, copy=True)
-    out[..., :2] = normalize_screen(x, w, h).cpu().numpy()
+    if kps.dtype == np.float64:
+        # float64 keypoints (3DPW; resolution 2 c_x / 2 c_y as float32 scalars)
+        x = torch.from_numpy(np.ascontiguousarray(kps[..., :2], dtype=np.float64)).to(device)
+        out[..., :2] = normalize_screen_f64(x, w, h).cpu().numpy()
+    else:
+        if not (float(w).is_integer() and float(h).is_integer()):
+            raise ValueError(f"float32 keypoints with a non-integral resolution {w} x {h}")
+        x = torch.from_numpy(np.ascontiguousarray(kps[..., :2], dtype=np.float32)).to(device)
+        out[..., :2] = normalize_screen(x, w, h).cpu().numpy()
     return out
 
 
@@ -54,6 +66,7 @@ def _world_to_camera(X: np.ndarray, R, t, device) -> np.ndarray:
 def load_dataset(name: str, data_dir: str, keypoints: str = "gt", device=None):
     """(dataset object, prepared split) of the reference's .npz files."""
     from common.datasets.CMUMocapDataset import CMUMocapDataset
+    from common.datasets.ThreeDPWDataset import ThreeDPWDataset
     from common.datasets.h36m_dataset import Human36mDataset
     from .cameras import h36m_camera_record
     from .npz_io import load_npz
@@ -63,8 +76,13 @@ def load_dataset(name: str, data_dir: str, keypoints: str = "gt", device=None):
     device = torch.device(device if device is not None else "cuda")
     path3d = os.path.join(data_dir, f"data_3d_{name}.npz")
     path2d = os.path.join(data_dir, f"data_2d_{name}_{keypoints}.npz")
-    cmu = name != "h36m"
-    dataset = CMUMocapDataset(path3d, use_3DPW=name == "CMU_3DPW") if cmu else Human36mDataset(path3d)
+    cmu = name in MOVING_CAMERA
+    if name == "3DPW":
+        dataset = ThreeDPWDataset(path3d)
+    elif cmu:
+        dataset = CMUMocapDataset(path3d, use_3DPW=name == "CMU_3DPW")
+    else:
+        dataset = Human36mDataset(path3d)
 
     # ---- 3D poses in camera space (run.py:65-81) ----
     for subject in dataset.subjects():

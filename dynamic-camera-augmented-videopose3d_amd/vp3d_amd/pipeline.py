@@ -52,6 +52,23 @@ def normalize_screen(x: torch.Tensor, w: int, h: int, out: Optional[torch.Tensor
     return out
 
 
+def normalize_screen_f64(x: torch.Tensor, w, h, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """X/w*2 - [1, h/w] on device for float64 keypoints and any (possibly float32,
+    non-integral) resolution -- the 3DPW path (ThreeDPWDataset.py:87-103, run.py:117):
+    the reference keeps the float64 result, which its generator later casts to float32
+    (run.py:458); the kernel computes the float64 expression and rounds once.  h / w is
+    evaluated here with the very objects given, so a float32 w, h keep the reference's
+    float32 division."""
+    _require_cuda(x, "x")
+    assert x.shape[-1] == 2
+    x = x.contiguous().double()
+    out = torch.empty(x.shape, dtype=torch.float32, device=x.device) if out is None else out
+    with torch.cuda.device(x.device):
+        N.check(N.load().vp3d_normalize_screen_f64(x.data_ptr(), x.numel() // 2, float(w), float(h / w),
+                                                   out.data_ptr(), _stream(x)))
+    return out
+
+
 def image_coordinates(x: torch.Tensor, w: int, h: int) -> torch.Tensor:
     _require_cuda(x, "x")
     assert x.shape[-1] == 2

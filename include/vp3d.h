@@ -312,6 +312,15 @@ int vp3d_seq_sliding_window(vp3d_seq_lifter* h, const float* x2d, const float* x
 int vp3d_normalize_screen(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,
                           void* stream);
 
+/* normalize_screen_coordinates on float64 keypoints with a non-integral resolution (the
+ * 3DPW path: keypoints stored f64, w = 2 c_x a float32 scalar, run.py:117 /
+ * ThreeDPWDataset.py:87-103): out = f32(X/w*2 - [1, hw]) with the whole expression in
+ * float64, i.e. the reference's float64 result rounded once when its generator casts the
+ * batch (run.py:458).  hw = the value h / w takes in the caller's arithmetic (float32
+ * division for float32 w, h). */
+int vp3d_normalize_screen_f64(const double* x, int64_t n_points, double w, double hw, float* out,
+                              void* stream);
+
 /* image_coordinates (camera.py:21-25): out = (X + [1, h/w]) * w / 2. */
 int vp3d_image_coordinates(const float* x, int64_t n_points, int32_t w, int32_t h, float* out,
                            void* stream);

@@ -393,9 +393,9 @@ def write_dataset_fixtures():
     np.savez_compressed(os.path.join(DATASET_DIR, "data_2d_CMU_gt.npz"), positions_2d=pos2, metadata=meta)
 
 
-def _ref_eval(actions, fw, channels, seed, use_generator):
+def _ref_eval(actions, fw, channels, seed, use_generator, jin=17, jout=17):
     """The reference's evaluate() numbers per action key (run.py:697-771)."""
-    m, sd, keys = build_ref_model(False, fw, channels=channels, seed=seed)
+    m, sd, keys = build_ref_model(False, fw, channels=channels, seed=seed, jin=jin, jout=jout)
     pad = (m.receptive_field() - 1) // 2
     out, e1_seq, infos, motion = {}, [], [], []
     for key, (cams, p3d, p2d) in actions.items():
@@ -506,7 +506,100 @@ def dataset_goldens():
     save("run_eval_datasets", **arrays)
 
 
-GROUPS = {"run_eval": run_eval_golden, "dataset": dataset_goldens, "model": model_goldens, "generator": generator_goldens,
+TDPW_SEQS = (("train", "courtyard_walk_00_0", 31, (1961.8529, 1969.2307, 540.0, 960.0)),
+             ("train", "downtown_car_01_1", 37, (1972.5, 1968.25, 541.25, 959.5)),
+             ("validation", "outdoors_turn_00_0", 29, (1961.8529, 1969.2307, 540.0, 960.0)))
+
+
+def _upsample_linear(x, factor=4):
+    """prepare_data_3dpw.py:29-37 (linear interpolation over time, float64 out)."""
+    from scipy.interpolate import interp1d
+    T = x.shape[0]
+    return interp1d(np.arange(T), x, axis=0, kind="linear")(np.linspace(0, T - 1, factor * T))
+
+
+def write_3dpw_fixture():
+    """A small dataset in the layout prepare_data_3dpw.py:58-103 writes: keyframe camera
+    poses (a yaw / pitch sweep and a walk) and SMPL joints upsampled 4x (so consecutive
+    extrinsics are NOT exactly orthogonal, as in the real data), camera-space joints,
+    float32 intrinsics (one with a non-integral principal point), float64 COCO 2D tracks."""
+    pos3, seqs, intr, pos2 = {}, {}, {}, {}
+    for subj, act, T0, (fx, fy, cx, cy) in TDPW_SEQS:
+        key = f"3dpw/{subj}/{act}"
+        for d in (pos3, seqs, intr, pos2):
+            d.setdefault(subj, {})
+        ang = np.cumsum(synth.uniform(21, key + "/ang", (T0, 3), -0.04, 0.04), axis=0)
+        E = np.zeros((T0, 3, 4), np.float32)
+        for t in range(T0):
+            a, b, c = ang[t]
+            Rz = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+            Ry = np.array([[np.cos(b), 0, np.sin(b)], [0, 1, 0], [-np.sin(b), 0, np.cos(b)]])
+            Rx = np.array([[1, 0, 0], [0, np.cos(c), -np.sin(c)], [0, np.sin(c), np.cos(c)]])
+            E[t, :, :3] = Rz @ Ry @ Rx
+        E[:, :, 3] = (np.cumsum(synth.normal(21, key + "/walk", (T0, 3), 0.02), axis=0)
+                      + np.array([0.0, 0.3, 3.5])).astype(np.float32)
+        cam_seq = _upsample_linear(E)
+        world = synth.gt_poses(22, key, T0, 24).astype(np.float32) * 2 + np.array([0.0, 0.0, 0.5], np.float32)
+        world = _upsample_linear(world.reshape(-1, 24, 3))
+        hom = np.concatenate([world, np.ones(world.shape[:2] + (1,), np.float32)], axis=2)
+        pos3[subj][act] = np.einsum("tij,tnj->tni", cam_seq, hom)
+        seqs[subj][act] = cam_seq
+        intr[subj][act] = np.array([[fx, 0, cx], [0, fy, cy], [0, 0, 1]], np.float32)
+        trk = synth.keypoint_tracks(23, key, T0, 18, int(2 * cx), int(2 * cy))
+        pos2[subj][act] = _upsample_linear(np.asarray(trk, np.float32))
+    meta = {"layout_name": "coco", "num_joints": 18,
+            "keypoints_symmetry": [[2, 3, 4, 8, 9, 10, 14, 16], [5, 6, 7, 11, 12, 13, 15, 17]]}
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_3d_3DPW.npz"), positions_3d=pos3, cam_seqs=seqs,
+                        cam_intrinsics=intr)
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_2d_3DPW_gt.npz"), positions_2d=pos2, metadata=meta)
+
+
+def dataset_3dpw_goldens():
+    """The reference's ThreeDPWDataset (ThreeDPWDataset.py:24-117, scipy logm) and run.py's
+    preparation (:65-124) on the 3DPW fixture, then its evaluation loop (generator as-is)."""
+    from common.datasets.ThreeDPWDataset import ThreeDPWDataset
+    os.makedirs(DATASET_DIR, exist_ok=True)
+    write_3dpw_fixture()
+    fw, channels, seed = [3, 3, 3], 256, 0
+    arrays = {}
+    ds = ThreeDPWDataset(os.path.join(DATASET_DIR, "data_3d_3DPW.npz"))
+    kp = np.load(os.path.join(DATASET_DIR, "data_2d_3DPW_gt.npz"), allow_pickle=True)["positions_2d"].item()
+    for subj in ds.subjects():
+        for act in ds[subj].keys():
+            anim = ds[subj][act]
+            pos = anim["positions"]
+            pos -= pos[:, :1]
+            anim["positions_3d"] = [pos]
+            cam = ds.cameras()[subj][act]
+            for k in ("cam_velocity", "cam_acceleration", "cam_angular_velocity", "cam_angular_acceleration"):
+                arrays[f"3dpw/{subj}/{act}/{k}"] = np.asarray(cam[k])
+            for k in ("center", "focal_length"):
+                arrays[f"3dpw/{subj}/{act}/{k}"] = np.asarray(cam["intrinsics"][k])
+            arrays[f"3dpw/{subj}/{act}/res"] = np.array([cam["intrinsics"]["res_w"], cam["intrinsics"]["res_h"]])
+    for subj in kp:
+        for act in kp[subj]:
+            k = kp[subj][act]
+            intr = ds.cameras()[subj][act]["intrinsics"]
+            k[..., :2] = ref_camera.normalize_screen_coordinates(k[..., :2], w=intr["res_w"], h=intr["res_h"])
+            kp[subj][act] = [k]
+    actions = {}
+    for subj in ds.subjects():
+        for act in ds[subj].keys():
+            c, p3, p2 = actions.setdefault(act.split(" ")[0], ([], [], []))
+            c.append(ds.cameras()[subj][act])
+            p3 += ds[subj][act]["positions_3d"]
+            p2 += kp[subj][act]
+            arrays[f"3dpw/{subj}/{act}/p3d"] = ds[subj][act]["positions_3d"][0]
+            arrays[f"3dpw/{subj}/{act}/kps"] = kp[subj][act][0]
+    res = _ref_eval(actions, fw, channels, seed, use_generator=True, jin=18, jout=24)
+    arrays["3dpw_actions"] = np.array(list(res.keys()))
+    arrays["3dpw_errors"] = np.stack(list(res.values()))
+    arrays["meta"] = np.array(json.dumps(dict(fw=fw, channels=channels, seed=seed,
+                                              seqs=[[s_, a_] for s_, a_, _, _ in TDPW_SEQS])))
+    save("run_eval_3dpw", **arrays)
+
+
+GROUPS = {"run_eval": run_eval_golden, "dataset": dataset_goldens, "dataset_3dpw": dataset_3dpw_goldens, "model": model_goldens, "generator": generator_goldens,
           "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens,
           "train": train_goldens, "seq_lifter": seq_lifter_goldens}
 

@@ -122,3 +122,72 @@ def test_run_main_dataset_matches_reference(name):
         print(name, k, got, v)
         assert abs(got[0] - v[0]) <= 1e-4, (k, got[0], v[0])          # Protocol #1, mm
         np.testing.assert_allclose(got[1:], v[1:], rtol=0, atol=1e-3)  # post-path protocols
+
+
+def _golden_3dpw():
+    g = np.load(os.path.join(GOLD, "run_eval_3dpw.npz"), allow_pickle=False)
+    return g, json.loads(str(g["meta"]))
+
+
+def test_3dpw_dataset_matches_reference():
+    """ThreeDPWDataset (ThreeDPWDataset.py:24-117) on the 3DPW fixture: per-sequence
+    normalised intrinsics and the camera-motion means (velocity, acceleration, angular
+    velocity from the matrix log of R_i^T R_{i+1}, angular acceleration) equal the
+    reference's, and the skeletons are COCO (18) / SMPL (24)."""
+    from common.datasets.ThreeDPWDataset import ThreeDPWDataset
+    g, meta = _golden_3dpw()
+    ds = ThreeDPWDataset(os.path.join(DATA, "data_3d_3DPW.npz"))
+    assert ds.skeleton_2d().num_joints() == 18 and ds.skeleton_3d().num_joints() == 24
+    assert ds.fps() == 60
+    n = 0
+    for subj, act in meta["seqs"]:
+        cam = ds.cameras()[subj][act]
+        key = f"3dpw/{subj}/{act}"
+        for k in ("center", "focal_length"):
+            got = np.asarray(cam["intrinsics"][k])
+            assert got.dtype == g[f"{key}/{k}"].dtype
+            np.testing.assert_array_equal(got, g[f"{key}/{k}"], err_msg=key + k)
+        np.testing.assert_array_equal([cam["intrinsics"]["res_w"], cam["intrinsics"]["res_h"]], g[key + "/res"])
+        for k in ("cam_velocity", "cam_acceleration", "cam_angular_velocity", "cam_angular_acceleration"):
+            np.testing.assert_allclose(cam[k], g[f"{key}/{k}"], rtol=1e-12, atol=1e-12, err_msg=key + k)
+        assert cam["extrinsics"].shape == (ds[subj][act]["positions"].shape[0], 3, 4)
+        n += 1
+    assert n == 3
+
+
+@pytest.mark.gpu
+def test_prepare_3dpw_matches_reference():
+    """run.py:65-124 for 3DPW on the device: root-zeroed camera-space 3D (float64, as the
+    reference keeps it) and the float64 keypoints normalised with the float32 resolution
+    2 c_x, 2 c_y (incl. a non-integral principal point), rounded once to float32 -- what the
+    reference's generator feeds the model (run.py:458)."""
+    from vp3d_amd.datasets import load_dataset
+    g, meta = _golden_3dpw()
+    _, data, _ = load_dataset("3DPW", DATA, "gt")
+    for subj, act in meta["seqs"]:
+        d = data[subj][act]
+        key = f"3dpw/{subj}/{act}"
+        np.testing.assert_array_equal(d["positions_3d"][0], g[key + "/p3d"], err_msg=key)
+        np.testing.assert_array_equal(d["keypoints"][0], g[key + "/kps"].astype(np.float32), err_msg=key)
+        assert d["cameras"][0]["extrinsics"].shape[0] == d["keypoints"][0].shape[0]
+        np.testing.assert_allclose(d["cameras"][0]["cam_angular_velocity"], g[key + "/cam_angular_velocity"],
+                                   rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_run_main_3dpw_matches_reference():
+    """`run.py -d 3DPW --evaluate` end to end (COCO 18 -> SMPL 24 joints, moving cameras,
+    per-sequence intrinsics) vs the reference's evaluation of the same files."""
+    import run
+    g, meta = _golden_3dpw()
+    want = dict(zip([str(a) for a in g["3dpw_actions"]], g["3dpw_errors"]))
+    res = run.main(["-d", "3DPW", "--data-dir", DATA, "-k", "gt", "--evaluate", "synthetic",
+                    "--fcn-architecture", ",".join(map(str, meta["fw"])), "--channels", str(meta["channels"]),
+                    "--seed", str(meta["seed"]), "--subjects-test", "*"])
+    assert set(res["per_action"]) == set(want)
+    for k, v in want.items():
+        got = np.asarray(res["per_action"][k])
+        print("3DPW", k, got, v)
+        assert abs(got[0] - v[0]) <= 1e-4, (k, got[0], v[0])          # Protocol #1, mm
+        np.testing.assert_allclose(got[1:], v[1:], rtol=0, atol=1e-3)  # post-path protocols
+    assert set(res["pmcc"]) >= {"cam_velocity", "cam_angular_velocity"}
