@@ -96,8 +96,8 @@ def build_parser():
     a('--data-dir', default='data', type=str, metavar='PATH',
       help='directory holding data_3d_<dataset>.npz and data_2d_<dataset>_<keypoints>.npz '
            '(the reference hard-codes /vol/bitbucket/bw1222/data/npz)')
-    a('--compute-dtype', default='fp32', choices=['fp32', 'bf16', 'fp16'],
-      help='arithmetic of the conv stack (fp32 = parity path)')
+    a('--compute-dtype', default='fp32', choices=['fp32', 'f16x3', 'bf16', 'fp16'],
+      help='arithmetic of the conv stack (fp32 = parity path; f16x3 = split fp16, fp32-level results on the 16-bit MFMAs)')
     a('--trust-checkpoint', action='store_true',
       help='allow full unpickling of a checkpoint you created yourself (by default only tensors, '
            'plain containers and the numpy RandomState of a run.py checkpoint are admitted)')

@@ -53,6 +53,8 @@ def load_data(args, stride=None):
     if args.dataset == "synthetic":
         data = synthetic_dataset(args)
     else:
+        if args.trajectory and args.dataset == "humaneva":
+            raise SystemExit("--trajectory needs camera intrinsics; HumanEva publishes none (humaneva_dataset.py)")
         _, data, _ = load_dataset(args.dataset, args.data_dir, args.keypoints)
     return downsample(data, args.downsample if stride is None else stride)
 

@@ -18,14 +18,16 @@ Per dataset, as run.py:65-124 prepares it:
                   motion means of ThreeDPWDataset.py:60-85).  3DPW keypoints are float64
                   with a float32 resolution 2 c_x, 2 c_y: normalised in float64 and
                   rounded once (vp3d_normalize_screen_f64).
-  h36m            one view per calibrated camera: world_to_camera(positions, R, t)
+  h36m, humaneva  one view per calibrated camera: world_to_camera(positions, R, t)
                   (vp3d_world_to_camera, bit-exact with the reference's torch-CPU qrot),
                   then joints 1.. made root-relative, the root keeping the trajectory;
                   2D tracks longer than the mocap are cut to its length (run.py:101-106);
                   keypoints normalised with each camera's resolution.  The camera record
                   is built from the static calibration (vp3d_amd.cameras.h36m_camera_record:
                   the quirk-Q1 fix — the reference's generators index the H36M 9-vector
-                  as a dict and crash), with zero camera motion.
+                  as a dict and crash), with zero camera motion.  HumanEva's record
+                  has extrinsics only (no published intrinsics: `intrinsics.unknown`),
+                  so it feeds the 2D-keypoint lifter, not the trajectory-conditioned one.
 Normalisation runs on the device (vp3d_normalize_screen: the reference's float64
 promotion rounded once to float32, quirk Q6).  Reading never unpickles code
 (vp3d_amd.npz_io).
@@ -38,7 +40,7 @@ import numpy as np
 import torch
 
 MOTION_KEYS = ("cam_velocity", "cam_acceleration", "cam_angular_velocity", "cam_angular_acceleration")
-DATASETS_3D = ("h36m", "CMU", "CMU_3DPW", "3DPW")
+DATASETS_3D = ("h36m", "humaneva", "CMU", "CMU_3DPW", "3DPW")
 MOVING_CAMERA = ("CMU", "CMU_3DPW", "3DPW")  # one view per action, per-frame extrinsics
 
 
@@ -68,7 +70,8 @@ def load_dataset(name: str, data_dir: str, keypoints: str = "gt", device=None):
     from common.datasets.CMUMocapDataset import CMUMocapDataset
     from common.datasets.ThreeDPWDataset import ThreeDPWDataset
     from common.datasets.h36m_dataset import Human36mDataset
-    from .cameras import h36m_camera_record
+    from common.datasets.humaneva_dataset import HumanEvaDataset
+    from .cameras import h36m_camera_record, world_to_camera_extrinsic
     from .npz_io import load_npz
 
     if name not in DATASETS_3D:
@@ -81,6 +84,8 @@ def load_dataset(name: str, data_dir: str, keypoints: str = "gt", device=None):
         dataset = ThreeDPWDataset(path3d)
     elif cmu:
         dataset = CMUMocapDataset(path3d, use_3DPW=name == "CMU_3DPW")
+    elif name == "humaneva":
+        dataset = HumanEvaDataset(path3d)
     else:
         dataset = Human36mDataset(path3d)
 
@@ -96,6 +101,8 @@ def load_dataset(name: str, data_dir: str, keypoints: str = "gt", device=None):
             else:
                 views = []
                 for cam in anim["cameras"]:
+                    if "orientation" not in cam:  # HumanEva S4: no calibration (the reference raises here too)
+                        raise ValueError(f"{name}: subject {subject} has 3D poses but uncalibrated cameras")
                     p = _world_to_camera(anim["positions"], cam["orientation"], cam["translation"], device)
                     p[:, 1:] -= p[:, :1]  # root keeps the trajectory
                     views.append(p)
@@ -145,7 +152,14 @@ def load_dataset(name: str, data_dir: str, keypoints: str = "gt", device=None):
             else:
                 cams = []
                 for cam_idx, cam in enumerate(dataset.cameras()[subject]):
-                    rec = h36m_camera_record(cam, views_3d[cam_idx].shape[0], normalized=True)
+                    if "focal_length" in cam:
+                        rec = h36m_camera_record(cam, views_3d[cam_idx].shape[0], normalized=True)
+                    else:
+                        # HumanEva: extrinsics only (the reference has no intrinsics for it)
+                        E = world_to_camera_extrinsic(cam["orientation"], cam["translation"])
+                        rec = {"intrinsics": {"focal_length": np.ones(2, np.float32),
+                                              "center": np.zeros(2, np.float32), "unknown": True},
+                               "extrinsics": np.repeat(E[None], views_3d[cam_idx].shape[0], axis=0)}
                     rec["intrinsics"]["res_w"], rec["intrinsics"]["res_h"] = cam["res_w"], cam["res_h"]
                     for k in MOTION_KEYS:
                         rec[k] = np.zeros(3)  # calibrated static cameras

@@ -599,7 +599,68 @@ def dataset_3dpw_goldens():
     save("run_eval_3dpw", **arrays)
 
 
-GROUPS = {"run_eval": run_eval_golden, "dataset": dataset_goldens, "dataset_3dpw": dataset_3dpw_goldens, "model": model_goldens, "generator": generator_goldens,
+HE_SEQS = (("Train/S1", "Walk 1 chunk0", 83), ("Train/S2", "Jog 1 chunk0", 71), ("Validate/S3", "Box 1 chunk1", 77))
+
+
+def write_humaneva_fixture():
+    """A small dataset in the upstream HumanEva layout (prepare_data_humaneva.py): world
+    15-joint mocap per (split/subject, action), three camera tracks of 2D keypoints
+    (640 x 480 pixels, one longer than the mocap)."""
+    pos3, pos2 = {}, {}
+    for subj, act, T in HE_SEQS:
+        key = f"he/{subj}/{act}"
+        root = np.cumsum(synth.normal(31, key + "/root", (T, 1, 3), 0.01), axis=0) + np.array([0.5, -0.2, 0.9])
+        body = synth.normal(31, key + "/body", (1, 15, 3), 0.25)
+        jit = synth.normal(31, key + "/jit", (T, 15, 3), 0.005)
+        pos3.setdefault(subj, {})[act] = (root + body + jit).astype(np.float32)
+        pos2.setdefault(subj, {})[act] = [synth.keypoint_tracks(32, f"{key}/{c}", T + (2 if c == 2 else 0), 15, 640, 480)
+                                          for c in range(3)]
+    meta = {"layout_name": "humaneva15", "num_joints": 15,
+            "keypoints_symmetry": [[2, 3, 4, 8, 9, 10], [5, 6, 7, 11, 12, 13]]}
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_3d_humaneva.npz"), positions_3d=pos3)
+    np.savez_compressed(os.path.join(DATASET_DIR, "data_2d_humaneva_gt.npz"), positions_2d=pos2, metadata=meta)
+
+
+def dataset_humaneva_goldens():
+    """The reference's HumanEvaDataset (humaneva_dataset.py:90-120) and run.py's
+    preparation of a calibrated multi-view dataset (:65-124: world_to_camera per camera,
+    root-relative joints, 2D cut to the mocap length and normalised per camera), then its
+    evaluation loop on edge-padded whole sequences (the reference's fetch_actions indexes
+    the per-subject camera list by action name and crashes, quirk Q1, as for H36M)."""
+    from common.datasets.humaneva_dataset import HumanEvaDataset
+    os.makedirs(DATASET_DIR, exist_ok=True)
+    write_humaneva_fixture()
+    fw, channels, seed = [3, 3, 3], 256, 0
+    arrays = {}
+    ds = HumanEvaDataset(os.path.join(DATASET_DIR, "data_3d_humaneva.npz"))
+    kp = np.load(os.path.join(DATASET_DIR, "data_2d_humaneva_gt.npz"), allow_pickle=True)["positions_2d"].item()
+    actions = {}
+    for subj, act, _ in HE_SEQS:
+        anim = ds[subj][act]
+        views3, views2 = [], []
+        for ci, cam in enumerate(anim["cameras"]):
+            p = ref_camera.world_to_camera(anim["positions"], R=cam["orientation"], t=cam["translation"])
+            p[:, 1:] -= p[:, :1]
+            k = kp[subj][act][ci][:p.shape[0]].copy()
+            k[..., :2] = ref_camera.normalize_screen_coordinates(k[..., :2], w=cam["res_w"], h=cam["res_h"])
+            views3.append(p)
+            views2.append(k)
+            arrays[f"he/{subj}/{act}/{ci}/p3d"] = p
+            arrays[f"he/{subj}/{act}/{ci}/kps"] = k
+        c, p3, p2 = actions.setdefault(act.split(" ")[0], ([], [], []))
+        c += [None] * len(views3)
+        p3 += views3
+        p2 += views2
+    res = _ref_eval(actions, fw, channels, seed, use_generator=False, jin=15, jout=15)
+    arrays["he_actions"] = np.array(list(res.keys()))
+    arrays["he_errors"] = np.stack(list(res.values()))
+    arrays["meta"] = np.array(json.dumps(dict(fw=fw, channels=channels, seed=seed,
+                                              seqs=[[s_, a_] for s_, a_, _ in HE_SEQS])))
+    save("run_eval_humaneva", **arrays)
+
+
+GROUPS = {"run_eval": run_eval_golden, "dataset": dataset_goldens, "dataset_3dpw": dataset_3dpw_goldens,
+          "dataset_humaneva": dataset_humaneva_goldens, "model": model_goldens, "generator": generator_goldens,
           "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens,
           "train": train_goldens, "seq_lifter": seq_lifter_goldens}
 

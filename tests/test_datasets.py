@@ -191,3 +191,63 @@ def test_run_main_3dpw_matches_reference():
         assert abs(got[0] - v[0]) <= 1e-4, (k, got[0], v[0])          # Protocol #1, mm
         np.testing.assert_allclose(got[1:], v[1:], rtol=0, atol=1e-3)  # post-path protocols
     assert set(res["pmcc"]) >= {"cam_velocity", "cam_angular_velocity"}
+
+
+def _golden_he():
+    g = np.load(os.path.join(GOLD, "run_eval_humaneva.npz"), allow_pickle=False)
+    return g, json.loads(str(g["meta"]))
+
+
+def test_humaneva_dataset_layout():
+    """HumanEvaDataset (humaneva_dataset.py:90-120): 15-joint skeleton, three calibrated
+    640x480 cameras per subject under every split prefix, translation in metres, S4
+    uncalibrated; the fixture's sequences keep their world-space mocap."""
+    from common.datasets.humaneva_dataset import HumanEvaDataset
+    g, meta = _golden_he()
+    ds = HumanEvaDataset(os.path.join(DATA, "data_3d_humaneva.npz"))
+    assert ds.skeleton_3d().num_joints() == 15 and ds.fps() == 60
+    cams = ds.cameras()
+    assert len(cams["Train/S1"]) == 3
+    for prefix in ("Train/", "Validate/", "Unlabeled/Train/", "Unlabeled/Validate/", "Unlabeled/"):
+        np.testing.assert_array_equal(cams[prefix + "S2"][1]["orientation"], cams["Train/S2"][1]["orientation"])
+    c = cams["Validate/S1"][0]
+    assert (c["res_w"], c["res_h"]) == (640, 480) and c["translation"].dtype == np.float32
+    np.testing.assert_allclose(c["translation"], np.array([4062.227, 663.2477, 1528.397], np.float32) / 1000)
+    assert cams["Train/S4"][0].get("orientation") is None
+    for subj, act in meta["seqs"]:
+        assert ds[subj][act]["positions"].shape[1:] == (15, 3)
+
+
+@pytest.mark.gpu
+def test_prepare_humaneva_matches_reference():
+    """run.py:65-124 for HumanEva on the device: per-camera world_to_camera, root-relative
+    joints, 2D cut to the mocap length and normalised -- bit-exact vs the reference."""
+    from vp3d_amd.datasets import load_dataset
+    g, meta = _golden_he()
+    _, data, _ = load_dataset("humaneva", DATA, "gt")
+    for subj, act in meta["seqs"]:
+        d = data[subj][act]
+        assert len(d["keypoints"]) == 3
+        for ci in range(3):
+            key = f"he/{subj}/{act}/{ci}"
+            np.testing.assert_array_equal(d["positions_3d"][ci], g[key + "/p3d"], err_msg=key)
+            np.testing.assert_array_equal(d["keypoints"][ci], g[key + "/kps"], err_msg=key)
+            assert d["cameras"][ci]["intrinsics"].get("unknown")
+
+
+@pytest.mark.gpu
+def test_run_main_humaneva_matches_reference():
+    import run
+    g, meta = _golden_he()
+    want = dict(zip([str(a) for a in g["he_actions"]], g["he_errors"]))
+    res = run.main(["-d", "humaneva", "--data-dir", DATA, "-k", "gt", "--evaluate", "synthetic",
+                    "--fcn-architecture", ",".join(map(str, meta["fw"])), "--channels", str(meta["channels"]),
+                    "--seed", str(meta["seed"]), "--subjects-test", "*"])
+    assert set(res["per_action"]) == set(want)
+    for k, v in want.items():
+        got = np.asarray(res["per_action"][k])
+        print("humaneva", k, got, v)
+        assert abs(got[0] - v[0]) <= 1e-4, (k, got[0], v[0])
+        np.testing.assert_allclose(got[1:], v[1:], rtol=0, atol=1e-3)
+    with pytest.raises(SystemExit):
+        run.main(["-d", "humaneva", "--data-dir", DATA, "--evaluate", "synthetic", "--trajectory"])
