@@ -744,27 +744,31 @@ def windows_main(args, world, rank, dev):
 
     if world == 1 and not args.no_extras:
         with torch.no_grad():
-            # ---- the parity-gate paths: exact fp32 and split fp16 (f16x3), same windows and B ----
+            # ---- the parity-gate paths: exact fp32 and split fp16 (f16x3), same windows and B
+            # (config 3: the f16x3 leg, its accurate dtype) ----
+            legs = [("f16x3", max(5, args.steps // 2))]
             if not traj:
-                for dt_acc, ksteps in (("fp32", max(3, args.steps // 4)), ("f16x3", max(5, args.steps // 2))):
-                    if dt_acc == dtype:
-                        continue
-                    ya = torch.empty_like(y)
-                    lifter.reserve(B, RF, dt_acc)
-                    dta, pla, doma = profiled_run(lifter, make_step(dt_acc, x, pairs, ya), ksteps, 1, 0.3, 1)
-                    yas = ya[idx].cpu().numpy()
-                    out[dt_acc] = {"value": round(G * ksteps / dta, 2), "unit": "poses/s", "steps": ksteps,
-                                   "ms_per_step": round(dta / ksteps * 1e3, 4),
-                                   "roofline": roofline_of(doma, PEAK_TFLOPS[dt_acc]),
-                                   "per_layer_ms": pla,
-                                   "mpjpe_delta_mm": abs(mp(yas) - mp(ref)) * 1e3,
-                                   "max_coord_delta_mm": float(np.abs(yas - ref).max()) * 1e3}
-                    parity[f"{dt_acc}_mpjpe_delta_mm"] = out[dt_acc]["mpjpe_delta_mm"]
-                    parity[f"{dt_acc}_max_coord_delta_mm"] = out[dt_acc]["max_coord_delta_mm"]
-                    del ya
-                if "f16x3" in out:
-                    out["f16x3"]["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per "
-                                                            "algorithmic multiply-add (hi.hi + hi.lo + lo.hi)")
+                legs.insert(0, ("fp32", max(3, args.steps // 4)))
+            for dt_acc, ksteps in legs:
+                if dt_acc == dtype:
+                    continue
+                ya = torch.empty_like(y)
+                lifter.reserve(B, RF, dt_acc)
+                dta, pla, doma = profiled_run(lifter, make_step(dt_acc, x, pairs, ya), ksteps, 1, 0.3, 1)
+                yas = ya[idx].cpu().numpy()
+                out[dt_acc] = {"value": round(G * ksteps / dta, 2), "unit": "poses/s", "steps": ksteps,
+                               "ms_per_step": round(dta / ksteps * 1e3, 4),
+                               "roofline": roofline_of(doma, PEAK_TFLOPS[dt_acc]),
+                               "per_layer_ms": pla,
+                               "mpjpe_delta_mm": abs(mp(yas) - mp(ref)) * 1e3,
+                               "max_coord_delta_mm": float(np.abs(yas - ref).max()) * 1e3}
+                parity[f"{dt_acc}_mpjpe_delta_mm"] = out[dt_acc]["mpjpe_delta_mm"]
+                parity[f"{dt_acc}_max_coord_delta_mm"] = out[dt_acc]["max_coord_delta_mm"]
+                del ya
+            if "f16x3" in out:
+                out["f16x3"]["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per "
+                                                        "algorithmic multiply-add (hi.hi + hi.lo + lo.hi)")
+            if not traj:
                 # ---- config-2 batch sweep (1 GPU) ----
                 sweep = {}
                 for Bs in args.sweep:

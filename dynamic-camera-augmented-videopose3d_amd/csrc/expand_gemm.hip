@@ -72,20 +72,39 @@ __device__ __forceinline__ void exp_vm() {
 // writes a slab lane-linearly (wave w: rows 16w .. 16w + 15); the permutation is applied
 // to the global source address.
 // RING: weight chunks resident (3: current, next, next-but-one; 2: current, next)
-template <typename CT, int NKS, int RB, bool GATHER, bool NT = false, int RING = 3>
-__global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
+// X3 (split fp16, VP3D_DTYPE_F16X3; CT = f16): the f32 input rows are split in registers
+// into hi = f16(x) and lo = f16(x - hi) fragments; the weights are Layer::wx3 (W 2^e as hi
+// and lo halves, each 32-wide K group [hi(32) | lo(32)], BN NOT folded), so a weight chunk
+// is 2 NKS slabs (hi, lo per k-slab) and each k-slab issues hi.hi + hi.lo + lo.hi; the
+// epilogue applies the BatchNorm as ATen does (x * scale, then + shift, two roundings) +
+// ReLU and writes the split output row (channel n at 64 (n / 32) + n % 32, lo 32 further):
+// 256 output bytes per row per 64-channel chunk, staged per wave and stored as 16-byte
+// pieces, 4 rows x 256 B per instruction.  One workgroup per CU (LDS), 4 waves.
+template <typename CT, int NKS, int RB, bool GATHER, bool NT = false, int RING = 3, bool X3 = false>
+__global__ __launch_bounds__(256, X3 ? 1 : 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
     constexpr int kRowsW = 16 * RB;
     constexpr int kRows = kRowsW * kExpWaves;
-    constexpr int kChunk = NKS * kExpSlab;
-    // ring of weight chunks, then per-wave output staging: kRowsW rows x 128 B, 16-byte
-    // unit c of row r at c ^ (r & 7)
-    __shared__ __attribute__((aligned(16))) char smem[RING * kChunk + kExpWaves * kRowsW * 128];
+    constexpr int NKW = X3 ? 2 * NKS : NKS;  // weight slabs per chunk
+    constexpr int kChunk = NKW * kExpSlab;
+    constexpr int kRowB = X3 ? 256 : 128;  // staged output bytes per row and chunk
+    // ring of weight chunks, then per-wave output staging: kRowsW rows x kRowB, 16-byte
+    // unit c of row r at c ^ (r & 7) (X3: c ^ (r & 15)); X3: then scale, shift (N floats each)
+    __shared__ __attribute__((aligned(16))) char smem[RING * kChunk + kExpWaves * kRowsW * kRowB +
+                                                      (X3 ? 2 * kExpMaxN * 4 : 0)];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int m_wave = blockIdx.x * kRows + wid * kRowsW;
-    u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * 128);
+    u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * kRowB);
+    float* const s_scale = (float*)(smem + RING * kChunk + kExpWaves * kRowsW * kRowB);
+    float* const s_shift = s_scale + kExpMaxN;
+    if constexpr (X3) {
+        for (int i = tid; i < p.N; i += 256) {
+            s_scale[i] = p.scale[i];
+            s_shift[i] = p.shift[i];
+        }
+    }
 
     // ---- weight chunk DMA: NKS pieces of 1 KB per wave ----
     const int dr = 16 * wid + (lane >> 2);
@@ -95,7 +114,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
         char* dst = smem + (chunk % RING) * kChunk + wid * 1024;
         const CT* src = wsrc + (int64_t)chunk * kExpChunkN * p.Kp;
 #pragma unroll
-        for (int q = 0; q < NKS; ++q)
+        for (int q = 0; q < NKW; ++q)
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + q * 32), (lds_ptr_t)(dst + q * kExpSlab), 16, 0, 0);
     };
     const int nchunks = p.N / kExpChunkN;
@@ -106,6 +125,22 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     // k = K, K + 1 are the bias columns (1.0), k > K + 1 zero ----
     const float* X = (const float*)p.A;
     u32x4 af[RB][NKS];
+    u32x4 afl[X3 ? RB : 1][NKS];  // X3: the lo fragments
+    constexpr float kBias = X3 ? 0.f : 1.f;  // the folded-shift column (16-bit path only)
+    auto put = [&](int rb, int ks, const float (&v)[8]) {
+        if constexpr (X3) {
+            f16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                h[e] = (f16)v[e];
+                l[e] = (f16)(v[e] - (float)h[e]);
+            }
+            af[rb][ks] = __builtin_bit_cast(u32x4, h);
+            afl[rb][ks] = __builtin_bit_cast(u32x4, l);
+        } else {
+            af[rb][ks] = pack8<CT>(v);
+        }
+    };
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
         int m = m_wave + rb * 16 + (lane & 15);
@@ -120,12 +155,12 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                 for (int e = 0; e < 8; e += 2) {
                     // K even: pairs are wholly in or out; out-of-range pairs read pair 0
                     const bool in = k0 + e < p.K;
-                    const float t = k0 + e == p.K ? 1.f : 0.f;
+                    const float t = k0 + e == p.K ? kBias : 0.f;
                     const float2 x = *(const float2*)(row + (in ? k0 + e : 0));
                     v[e] = in ? x.x : t;
                     v[e + 1] = in ? x.y : t;
                 }
-                af[rb][ks] = pack8<CT>(v);
+                put(rb, ks, v);
             }
         } else {
             // window b starts at sequence frame start_b - lead; row t covers window frames
@@ -156,13 +191,13 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                             v[e + 1] = x.y;
                         } else {
                             const bool in = k < p.K;
-                            const float t1 = k == p.K ? 1.f : 0.f;
+                            const float t1 = k == p.K ? kBias : 0.f;
                             const float2 x = *(const float2*)(row + (in ? k : 0));
                             v[e] = in ? x.x : t1;
                             v[e + 1] = in ? x.y : t1;
                         }
                     }
-                    af[rb][ks] = pack8<CT>(v);
+                    put(rb, ks, v);
                 }
                 continue;
             }
@@ -178,7 +213,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                     // lda, f2 and K even: a pair never straddles a tap or the kps|cams edge
                     const int k = k0 + e;
                     const bool in = k < p.K;
-                    const float t1 = k == p.K ? 1.f : 0.f;
+                    const float t1 = k == p.K ? kBias : 0.f;
                     const int tap = in ? (int)(((float)k + 0.5f) * inv_lda) : 0;
                     const int c = in ? k - tap * p.lda : 0;
                     int fr = f0 + tap;
@@ -189,7 +224,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                     v[e] = in ? tv.x : t1;
                     v[e + 1] = in ? tv.y : t1;
                 }
-                af[rb][ks] = pack8<CT>(v);
+                put(rb, ks, v);
             }
         }
     }
@@ -215,6 +250,83 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
         if (ch + RING - 1 < nchunks) stage_w(ch + RING - 1);
         const char* wb = smem + (ch % RING) * kChunk;
         f32x4 acc[RB][4];
+        if constexpr (X3) {
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                u32x4 wh[4], wl[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    wh[j] = *(const u32x4*)(wb + (2 * ks) * kExpSlab + j * 1024 + frag_off);
+                    wl[j] = *(const u32x4*)(wb + (2 * ks + 1) * kExpSlab + j * 1024 + frag_off);
+                }
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[rb][j] = mfma16<CT>(wh[j], af[rb][ks], ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[rb][j]);
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[rb][j] = mfma16<CT>(wh[j], afl[rb][ks], acc[rb][j]);
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[rb][j] = mfma16<CT>(wl[j], af[rb][ks], acc[rb][j]);
+            }
+            // epilogue: BN affine (two roundings) + ReLU, split into hi / lo, staged per row
+            const int n0 = ch * kExpChunkN;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int nl = j * 16 + (lane >> 4) * 4;
+                const f32x4 sc = *(const f32x4*)&s_scale[n0 + nl];
+                const f32x4 sh = *(const f32x4*)&s_shift[n0 + nl];
+                const int uh = (nl >> 5) * 8 + ((nl & 31) >> 3);
+                const int half = (nl >> 2) & 1;
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) {
+                    f16 h[4], l[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float v = __fadd_rn(__fmul_rn(acc[rb][j][r], sc[r]), sh[r]);
+                        if (p.relu) v = v > 0.f ? v : 0.f;
+                        h[r] = (f16)v;
+                        l[r] = (f16)(v - (float)h[r]);
+                    }
+                    const int row = rb * 16 + (lane & 15);
+                    char* base = (char*)stage + row * 256 + (half << 3);
+                    typedef f16 f16x4 __attribute__((ext_vector_type(4)));
+                    *(f16x4*)(base + ((uh ^ (row & 15)) << 4)) = f16x4{h[0], h[1], h[2], h[3]};
+                    *(f16x4*)(base + (((uh + 4) ^ (row & 15)) << 4)) = f16x4{l[0], l[1], l[2], l[3]};
+                }
+            }
+            asm volatile("" ::: "memory");
+            // 16 lanes per row, 4 rows per instruction: 256 B of a row (2 whole lines)
+#pragma unroll
+            for (int q = 0; q < 4 * RB; ++q) {
+                const int row = q * 4 + (lane >> 4);
+                const int c16 = lane & 15;
+                const u32x4 v = stage[row * 16 + (c16 ^ (row & 15))];
+                const int m = m_wave + row;
+                if (m < p.M) {
+                    u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + c16 * 8);
+                    if constexpr (NT)
+                        __builtin_nontemporal_store(v, dst);
+                    else
+                        *dst = v;
+                }
+            }
+            asm volatile("" ::: "memory");
+            if (ch + 1 < nchunks) {
+                if (m_wave + kRowsW > p.M)
+                    exp_vm<0>();
+                else if (RING == 3 && ch + 2 < nchunks)
+                    exp_vm<NKW + 4 * RB>();
+                else
+                    exp_vm<4 * RB>();
+            }
+            __builtin_amdgcn_s_barrier();
+            continue;
+        }
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             u32x4 wf[4];
@@ -282,15 +394,15 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     }
 }
 
-template <typename CT, int RB, bool GATHER, bool NT, int RING = 3>
+template <typename CT, int RB, bool GATHER, bool NT, int RING = 3, bool X3 = false>
 hipError_t launch_rb_nt(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
     const dim3 grid((p.M + 64 * RB - 1) / (64 * RB));
     switch (nks) {
-        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
-        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
-        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
-        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
-        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB, GATHER, NT, RING>), grid, dim3(256), 0, s, p, g); break;
+        case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER, NT, RING, X3>), grid, dim3(256), 0, s, p, g); break;
+        case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER, NT, RING, X3>), grid, dim3(256), 0, s, p, g); break;
+        case 3: hipLaunchKernelGGL((expand_gemm_h16<CT, 3, RB, GATHER, NT, RING, X3>), grid, dim3(256), 0, s, p, g); break;
+        case 4: hipLaunchKernelGGL((expand_gemm_h16<CT, 4, RB, GATHER, NT, RING, X3>), grid, dim3(256), 0, s, p, g); break;
+        case 5: hipLaunchKernelGGL((expand_gemm_h16<CT, 5, RB, GATHER, NT, RING, X3>), grid, dim3(256), 0, s, p, g); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -364,6 +476,31 @@ hipError_t launch_expand_gemm_gather(const ConvGemmParams& p, const GatherSrc& g
                                      hipStream_t stream) {
     const int nks = (p.K + 2 + 31) / 32;
     return compute == Act::BF16 ? launch_t<bf16, true>(p, g, nks, stream) : launch_t<f16, true>(p, g, nks, stream);
+}
+
+// Split-fp16 expand (X3): p.W = Layer::wx3 with p.Kp its row pitch in halves (2 Kp), the
+// scale / shift unfolded (scale_x3, shift), p.ldy the split output pitch in halves (2 N).
+bool expand_gemm_x3_eligible(const ConvGemmParams& p, const GatherSrc* g) {
+    if (p.Ktap != p.K || p.dil != 1) return false;
+    const int nks = (p.K + 31) / 32;
+    if (nks < 1 || nks > 5 || 2 * nks * 32 > p.Kp) return false;
+    if (p.K % 2 || p.lda % 2 || (!g && (reinterpret_cast<uintptr_t>(p.A) & 7))) return false;
+    if (p.N % kExpChunkN || p.N > kExpMaxN || p.ldy % 8 || (reinterpret_cast<uintptr_t>(p.Y) & 15)) return false;
+    if (g && (g->f2 % 2 || (reinterpret_cast<uintptr_t>(g->kps) & 7) ||
+              (g->cams && (reinterpret_cast<uintptr_t>(g->cams) & 7)) || p.lda != g->f2 + (g->cams ? 12 : 0)))
+        return false;
+    return p.R == nullptr && p.M > 0;
+}
+
+hipError_t launch_expand_gemm_x3(const ConvGemmParams& p, const GatherSrc* g, hipStream_t stream) {
+    const int nks = (p.K + 31) / 32;
+    const bool nt = (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
+    const GatherSrc none{};
+    if (g)
+        return nt ? launch_rb_nt<f16, 2, true, true, 3, true>(p, *g, nks, stream)
+                  : launch_rb_nt<f16, 2, true, false, 3, true>(p, *g, nks, stream);
+    return nt ? launch_rb_nt<f16, 2, false, true, 3, true>(p, none, nks, stream)
+              : launch_rb_nt<f16, 2, false, false, 3, true>(p, none, nks, stream);
 }
 
 }  // namespace vp3d

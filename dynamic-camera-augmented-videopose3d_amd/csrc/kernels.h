@@ -85,6 +85,12 @@ bool expand_gather_eligible(const ConvGemmParams& p, const GatherSrc& g, Act out
 hipError_t launch_expand_gemm_gather(const ConvGemmParams& p, const GatherSrc& g, Act compute,
                                      hipStream_t stream);
 
+// Split-fp16 expand conv (VP3D_DTYPE_F16X3): f32 input rows (or the gather of `g`) split
+// into hi / lo halves in registers, Layer::wx3 weights, BN + ReLU in the epilogue, split
+// output rows (expand_gemm.hip, X3 mode).
+bool expand_gemm_x3_eligible(const ConvGemmParams& p, const GatherSrc* g);
+hipError_t launch_expand_gemm_x3(const ConvGemmParams& p, const GatherSrc* g, hipStream_t stream);
+
 // Tile geometry the packer must pad to (rows of W to kPadN, K to kPadK).
 constexpr int kPadN = 256;
 constexpr int kPadK = 64;

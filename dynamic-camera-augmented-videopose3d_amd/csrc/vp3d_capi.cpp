@@ -560,6 +560,21 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
             p.W = L.w32;
             e = launch_conv_gemm(p, Act::F32, Act::F32, Act::F32, s);
             launched = true;
+        } else if (x3 && first && nl > 2 && [&] {
+                       ConvGemmParams q = p;
+                       q.W = L.wx3;
+                       q.Kp = 2 * L.Kp;
+                       q.ldy = 2 * L.cout;
+                       return expand_gemm_x3_eligible(q, gs);
+                   }()) {
+            // split-fp16 expand: the f32 rows (window gather + camera concat fused) split in
+            // registers, BN + ReLU in the epilogue, split output rows (expand_gemm.hip)
+            p.W = L.wx3;
+            p.Kp = 2 * L.Kp;
+            p.scale = L.scale_x3;
+            p.ldy = 2 * L.cout;
+            e = launch_expand_gemm_x3(p, gs, s);
+            launched = true;
         } else if (x3) {
             // split fp16: three 16-bit MFMA products per K group on conv_gemm_q64 (X3 mode)
             if (first) {
@@ -672,6 +687,10 @@ int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const flo
     if (!kps || !seq_off || !seq_len || !pairs || !y) return fail(VP3D_ERR_ARG, "a device pointer is NULL");
     if (B <= 0) return fail(VP3D_ERR_ASSERT, "batch must be positive");
     if (dtype < 0 || dtype > VP3D_DTYPE_F16X3) return fail(VP3D_ERR_ARG, "unknown dtype");
+    // bf16's 8-bit mantissa on the metre-scale K.E channels: 30 mm errors on the config-3
+    // windows; the camera-conditioned pipeline takes fp16, f16x3 or fp32
+    if (cams && dtype == VP3D_DTYPE_BF16)
+        return fail(VP3D_ERR_ARG, "bf16 is refused with the camera concat (use fp16, f16x3 or fp32)");
     const int cin = h->cfg.num_joints_in * h->cfg.in_features;
     if (f2 + (cams ? 12 : 0) != cin)
         return fail(VP3D_ERR_ASSERT, "frame features (" + std::to_string(f2) + (cams ? " + 12" : "") +

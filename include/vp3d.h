@@ -129,7 +129,9 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
  *   seq_off: device int64 first frame of each sequence; seq_len: device int32
  *   pairs:   device int32 (B, 2) = (sequence, start); window b = sequence frames
  *            [start - lead, start - lead + window), clamped to [0, len-1]
- *   y:       device f32 (B, vp3d_out_frames(window), J_out, 3) */
+ *   y:       device f32 (B, vp3d_out_frames(window), J_out, 3)
+ * With cams, dtype VP3D_DTYPE_BF16 is refused (VP3D_ERR_ARG): its 8-bit mantissa on the
+ * metre-scale K.E channels costs ~30 mm; fp16, f16x3 (the accurate fast path) or f32. */
 int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const float* cams,
                          const int64_t* seq_off, const int32_t* seq_len, const int32_t* pairs, int B,
                          int window, int lead, float* y, int dtype, void* stream);

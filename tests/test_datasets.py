@@ -190,7 +190,7 @@ def test_run_main_3dpw_matches_reference():
         print("3DPW", k, got, v)
         assert abs(got[0] - v[0]) <= 1e-4, (k, got[0], v[0])          # Protocol #1, mm
         np.testing.assert_allclose(got[1:], v[1:], rtol=0, atol=1e-3)  # post-path protocols
-    assert set(res["pmcc"]) >= {"cam_velocity", "cam_angular_velocity"}
+    assert res["pmcc"] == {}  # the reference's PMCC rows need >= 6 sequences (vp3d_amd.evaluate)
 
 
 def _golden_he():

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import make_model, mpjpe_np
+from helpers import H16_TOL, make_model, mpjpe_np
 from oracle.temporal_ref import lifter_forward
 from vp3d_amd import synth
 
@@ -21,10 +21,6 @@ pytestmark = pytest.mark.gpu
 
 FP32_COORD_TOL = 1e-5
 FP32_MPJPE_TOL = 1e-7
-H16_TOL = {  # (max |coordinate delta|, |dMPJPE|) in metres; measured maxima (MI355X, round 2):
-    "bf16": (1.0e-2, 1.5e-4),  # 3.56 mm (dilated 20,242-frame sequence), 0.057 mm
-    "fp16": (1.2e-3, 2.0e-5),  # 0.35 mm (B = 2050), 0.0058 mm
-}
 
 
 def _run(strided, B, T, fw=(3, 3, 3, 3, 3), causal=False, channels=1024, jin=17, jout=17,

@@ -42,11 +42,15 @@ def split(x):
     return hi, h16((x - hi) * LO_SCALE)
 
 
+W3 = False  # a third weight half: W s = Wh + Wl + W3 exactly, and a 4th product A_hi . W3
+
+
 def wsplit(W):
     e = 14 - int(np.floor(np.log2(float(W.abs().max()))))
     Ws = W * (2.0 ** e)
     Wh = h16(Ws)
-    return Wh, h16(Wh / LO_SCALE), h16(Ws - Wh), 2.0 ** -e
+    Wl = h16(Ws - Wh)
+    return Wh, h16(Wh / LO_SCALE), Wl, (h16(Ws - Wh - Wl) if W3 else None), 2.0 ** -e
 
 
 def emulate(sd, x, fw, eps=1e-5):
@@ -59,10 +63,12 @@ def emulate(sd, x, fw, eps=1e-5):
 
     def conv(pair, wname, stride):
         hi, lo = pair
-        Wh, Wh11, Wl, inv_s = wsplit(sdt[wname])
+        Wh, Wh11, Wl, Wr, inv_s = wsplit(sdt[wname])
         acc = F.conv1d(hi, Wh, None, stride=stride)
         acc = acc + F.conv1d(lo, Wh11, None, stride=stride)
         acc = acc + F.conv1d(hi, Wl, None, stride=stride)
+        if Wr is not None:
+            acc = acc + F.conv1d(hi, Wr, None, stride=stride)
         return acc, inv_s
 
     def bn_relu(acc, inv_s, name):
@@ -88,18 +94,44 @@ def emulate(sd, x, fw, eps=1e-5):
     return y.permute(0, 2, 1).reshape(B, -1, 17, 3).numpy()
 
 
+def dolly_windows(B, seed=1000, n_seq=64, L=2048, W=243):
+    """vp3d_amd.pipeline.SyntheticWindowPool(cameras=True) windows on the host: normalised
+    random-walk tracks + K.E (CMU K, yaw + dolly extrinsics), edge-clamped."""
+    pairs = np.random.RandomState(seed + 1)
+    seqs = pairs.randint(0, n_seq, size=B)
+    starts = pairs.randint(0, L, size=B)
+    K = np.diag([1.5625, 1.5625, 1.0]).astype(np.float32)
+    out = np.zeros((B, W, 46), np.float32)
+    cache = {}
+    for b in range(B):
+        i = int(seqs[b])
+        if i not in cache:
+            trk = synth.keypoint_tracks(seed, f"pool{i}", L)
+            kps = (trk / 1280 * 2 - np.array([1, 720 / 1280])).astype(np.float32).reshape(L, 34)
+            ke = (K @ synth.camera_extrinsics(seed, f"pool{i}", L)).astype(np.float32).reshape(L, 12)
+            cache[i] = np.concatenate([kps, ke], axis=1)
+        f = np.clip(np.arange(W) + starts[b] - (W - 1) // 2, 0, L - 1)
+        out[b] = cache[i][f]
+    return out.reshape(B, W, 23, 2)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=64)
     ap.add_argument("--traj", action="store_true")
     ap.add_argument("--lo-scale", type=float, default=1.0)
+    ap.add_argument("--dolly", action="store_true", help="the bench's config-3 windows (K.E up to ~22 m)")
+    ap.add_argument("--w3", action="store_true", help="three weight halves, four products")
     a = ap.parse_args()
-    global LO_SCALE
-    LO_SCALE = a.lo_scale
+    global LO_SCALE, W3
+    LO_SCALE, W3 = a.lo_scale, a.w3
     fw = [3, 3, 3, 3, 3]
-    jin = 23 if a.traj else 17
+    jin = 23 if (a.traj or a.dolly) else 17
     sd = synth.lifter_state_dict(keys_shapes(jin, fw, 1024), seed=0)
-    x = synth.normalized_windows(1, "x64_243", a.B, 243, n_joints=jin)
+    if a.dolly:
+        x = dolly_windows(a.B)
+    else:
+        x = synth.normalized_windows(1, "x64_243", a.B, 243, n_joints=jin)
     ref = lifter_forward(sd, x, fw, strided=True).numpy()
     ref64 = lifter_forward(sd, x, fw, strided=True, dtype=torch.float64).numpy()
     y = emulate(sd, x, fw)
