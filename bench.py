@@ -157,6 +157,7 @@ def stream_main(args, world, rank, dev):
     n_w = sum(v.size for k, v in sd.items() if (k.startswith("layers_conv") or k.startswith("expand_conv")
                                                  or k == "shrink.weight") and k.endswith("weight"))
     step_bytes = n_w * wbytes
+    step_flop = 2 * n_w  # one multiply-add per weight per step (algorithmic; 33,867,776 FLOP at 1024 ch)
     step_s = ev_ms * 1e-3 / args.steps
     achieved = step_bytes / step_s / 1e9
     # parity: first 64 frames of a stream vs the whole-sequence causal evaluation
@@ -175,6 +176,17 @@ def stream_main(args, world, rank, dev):
         e1.record()
         e1.synchronize()
         lat.append(e0.elapsed_time(e1) * 1e3)
+    # real-time serving, ONE frame in flight: host frame in -> host pose out, wall clock
+    serve_lat = None
+    if mode == "pipe":
+        frames_h = xs[0].cpu().numpy()
+        serve_lat = []
+        with st.serve(idle_ms=200.0) as sv:
+            for i in range(32 + 512):
+                t0 = time.perf_counter_ns()
+                sv.step(frames_h[i % T])
+                if i >= 32:  # after the first frames (weights to VGPRs, clocks up)
+                    serve_lat.append((time.perf_counter_ns() - t0) * 1e-3)
     pad = (RF_FULL - 1) // 2
     xp = torch.cat([xs[:, :1].expand(1, 2 * pad, -1, -1), xs], dim=1).cpu()
     ref = lifter_forward(sd, xp, FW, causal=True).numpy()[0]
@@ -202,23 +214,39 @@ def stream_main(args, world, rank, dev):
                                   "persist": " (one persistent launch: every CU runs every layer, weights in LDS)",
                                   "launches": " (10 GEMV launches per step)"}[mode],
                    "frames_per_step": 1, "steps_per_graph": G, "mode": mode, "parallelism": f"replicas{world}"},
-        "roofline": {"bound": "hbm", "kernel": {"pipe": "stream_pipe_kernel", "persist": "stream_persist_kernel",
-                                                "launches": "stream step (10 stream_gemv launches)"}[mode],
-                     "note": "achieved = the step's weight bytes / step time: the unit of work of a "
-                             "weight-streaming step, whose 8 TB/s roofline is "
-                             f"{step_bytes / 8e12 * 1e6:.2f} us/step. "
-                             + ({"pipe": "Here the weights stay resident in VGPRs (persist: LDS) for the whole "
-                                         "launch, so frac > 1 is possible: the step period is set by the "
-                                         "inter-CU hand-off latency of the layer pipeline, not by HBM.",
-                                 "persist": "Here the weights stay resident in LDS for the whole launch, so "
-                                            "frac > 1 is possible: the step is bound by the hand-off latency "
-                                            "between layers, not by HBM.",
-                                 "launches": "The weights are re-read every step."}[mode]),
-                     "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
-                     "frac": round(achieved / 8000.0, 4), "traffic": None,
-                     "bytes_per_step": step_bytes, "avg_step_us": round(step_s * 1e6, 3)},
+        # the bound that applies: with the weights resident on chip (pipe: VGPRs, persist: LDS)
+        # a step is FMA work (f16 x f32 + f32, v_fma_mix_f32) spread over the CUs and chained
+        # through 10 layer hand-offs -- priced here against the f32 vector FMA peak; the
+        # weight-streaming (HBM) view is kept beside it for the GEMV form
+        "roofline": {"bound": "valu" if mode != "launches" else "hbm",
+                     "kernel": {"pipe": "stream_pipe_kernel", "persist": "stream_persist_kernel",
+                                "launches": "stream step (10 stream_gemv launches)"}[mode],
+                     "achieved": round(step_flop / step_s / 1e12, 3) if mode != "launches" else round(achieved, 1),
+                     "peak": 157.3 if mode != "launches" else 8000.0,
+                     "unit": "TFLOP/s" if mode != "launches" else "GB/s",
+                     "frac": round(step_flop / step_s / 1e12 / 157.3, 4) if mode != "launches"
+                     else round(achieved / 8000.0, 4),
+                     "traffic": None, "flop_per_step": step_flop, "avg_step_us": round(step_s * 1e6, 3),
+                     "note": ("achieved = the step's algorithmic FLOP (2 x MACs of the 10 convs) / the pipelined "
+                              "step time (frames of a 64-step graph flowing through the layer groups); peak = "
+                              "the f32 vector peak (157.3 TF spec; the unpacked v_fma_mix_f32 the kernel issues "
+                              "runs at half of it). The per-frame floor is the hand-off chain: one frame crosses "
+                              "10 layer groups (serve_latency_us)." if mode != "launches" else
+                              "weights re-read every step: HBM-bound GEMVs"),
+                     "hbm_view": {"bytes_per_step": step_bytes, "achieved_GBps": round(achieved, 1),
+                                  "frac_of_8TBps": round(achieved / 8000.0, 4)}},
         "cpu_baseline": cpu,
-        "single_step_latency_us": round(float(np.median(lat)), 2),
+        "single_step_latency_us": round(float(np.median(serve_lat if serve_lat else lat)), 2),
+        "single_step_latency_note": ("serve form: one frame in flight, host frame posted to pinned memory -> pose "
+                                     "back in host memory, wall clock, median of 512 (resident launch, "
+                                     "vp3d_stream_serve_*)" if serve_lat else
+                                     "eager launch of one step from an idle stream (HIP events)"),
+        "serve_latency_us": ({"median": round(float(np.median(serve_lat)), 2),
+                              "p90": round(float(np.percentile(serve_lat, 90)), 2),
+                              "p99": round(float(np.percentile(serve_lat, 99)), 2),
+                              "frames_per_s_one_in_flight": round(1e6 / float(np.median(serve_lat)), 1)}
+                             if serve_lat else None),
+        "eager_step_latency_us": round(float(np.median(lat)), 2),
         "parity": {"frames": T, f"{args.dtype}_max_coord_delta_mm": float(np.abs(outs - ref).max()) * 1e3,
                    f"{args.dtype}_mpjpe_delta_mm": abs(mp(outs) - mp(ref)) * 1e3},
     }

@@ -183,6 +183,19 @@ struct StreamPipeParams {
     float* state;                          // [workgroups][state_stride]: k-conv rings / expand history
     int state_stride;
     int steps;
+    // serve form (vp3d_stream_serve_*): the launch stays resident and takes frames as the
+    // host posts them -- `frames` / `poses` are then host-mapped rings, frame t is readable
+    // once *posted > t, and the shrink workgroups report frame t done by done_host[i] = t + 1
+    // (i = shrink workgroup).  The expand role ends the launch at the first frame not posted
+    // within idle_ticks (100 MHz clock) or once *stop is set, by writing it to *end_frame
+    // (device word, all ones while serving); every other role leaves when it reaches that frame.
+    int serve;
+    const unsigned* posted;
+    const unsigned* stop;
+    unsigned* end_frame;
+    unsigned* done_host;
+    unsigned* ended_host;                  // host-mapped copy of the end frame + 1 (0 while serving)
+    unsigned long long idle_ticks;
 };
 int stream_pipe_lds_bytes(int C, int cin0, int max_ring);
 bool stream_pipe_channels_ok(int C);

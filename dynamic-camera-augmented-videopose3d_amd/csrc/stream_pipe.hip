@@ -90,8 +90,13 @@ __device__ __forceinline__ void pref_issue(Pref& r, const gu64* g, int n, int ti
         if (tid + j * kThreads < n) r.v[j] = __hip_atomic_load(g + tid + j * kThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// true once every granule carried `tag`; false on timeout (sets the fault words) or when
+// another wave aborted, or -- serve form -- once the launch ended before frame tag - 1
+// (*end < tag: that frame is never produced; *ended is then set)
 __device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* x, volatile int* abort_flag,
-                            const StreamFault& f, int tid) {
+                            const StreamFault& f, int tid, unsigned long long limit = 0,
+                            const unsigned* end = nullptr, volatile int* ended = nullptr) {
+    if (limit == 0) limit = f.spin_ticks;
     unsigned pending = 0;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -109,7 +114,11 @@ __device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* 
             start = __builtin_amdgcn_s_memrealtime();
         } else {
             if (*abort_flag) return false;
-            if (__builtin_amdgcn_s_memrealtime() - start > f.spin_ticks) {
+            if (end && __hip_atomic_load(end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tag) {
+                *ended = 1;
+                return false;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - start > limit) {
                 *abort_flag = 1;
                 __hip_atomic_store((gu32*)f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (f.err_host) __hip_atomic_store(f.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -193,10 +202,14 @@ template <typename WT, int KS>
 __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipeParams p) {
     constexpr int CWK = kPipeCwK, CWP = kPipeCwP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ int abort_flag;
+    __shared__ int abort_flag, end_flag;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wg = blockIdx.x;
     const int C = p.C, nb = p.nb, nl = p.nl, Q = p.queue;
+    // serve form: downstream waits also watch the end word and may last the expand role's
+    // idle budget (frames arrive at the host's pace)
+    const unsigned* const endw = p.serve ? p.end_frame : nullptr;
+    const unsigned long long limit = p.serve ? p.fault.spin_ticks + p.idle_ticks : p.fault.spin_ticks;
     const int nE = 2 * nb + 1;
     // per-role parameters selected with compile-time indices (a runtime index into the
     // by-value kernel argument would copy it to scratch)
@@ -234,7 +247,10 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             d = p.dil[q];
             R = p.ring[q];
         }
-    if (tid == 0) abort_flag = 0;
+    if (tid == 0) {
+        abort_flag = 0;
+        end_flag = 0;
+    }
 
     // ---- LDS carve ----
     float* xbuf = (float*)smem;               // 2 x C: swept input vector, by frame parity
@@ -274,12 +290,41 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = 2 * i < K0 ? src[i] : 0u;  // K0 <= kPipeExpandK
         }
         const float sc = c < c_hi ? scl[c - c_lo] : 0.f, sh = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
-        for (int s = 0; s < p.steps; ++s) {
+        for (int s = 0;; ++s) {
             const int t = t0 + s;
+            if (!p.serve) {
+                if (s >= p.steps) break;
+            } else {
+                // serve: wait for frame t to be posted; end the launch on a stop request or
+                // after idle_ticks without it
+                if (tid == 0) {
+                    bool go = false;
+                    const unsigned long long start = __builtin_amdgcn_s_memrealtime();
+                    for (;;) {
+                        if (__hip_atomic_load(p.posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) > (unsigned)t) {
+                            go = true;
+                            break;
+                        }
+                        if (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                            __builtin_amdgcn_s_memrealtime() - start > p.idle_ticks)
+                            break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    if (!go) {
+                        __hip_atomic_store(p.end_frame, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(p.ended_host, (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                    end_flag = go ? 0 : 1;
+                }
+                __syncthreads();
+                if (end_flag) break;
+            }
             float* xv = xin + (s & 1) * kPipeExpandK;
             const float* fr = p.frames + (int64_t)(t & (Q - 1)) * cin0;
             for (int i = tid; i < cin0; i += kThreads) {
-                const float v = fr[i];
+                const float v = p.serve ? __uint_as_float(__hip_atomic_load((const unsigned*)fr + i, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_SYSTEM))
+                                        : fr[i];
                 const float h1 = t == 0 ? v : hist[i];                          // frame t-1
                 const float h2 = t <= 1 ? (t == 0 ? v : h1) : hist[cin0 + i];   // frame t-2
                 xv[i] = h2;
@@ -323,13 +368,17 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         }
         Pref pf;
         pref_issue(pf, edge(role - 1, t0), C, tid);
-        for (int s = 0; s < p.steps; ++s) {
+        for (int s = 0; p.serve || s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
-            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid)) abort_flag = 1;
+            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, limit, endw,
+                             &end_flag) &&
+                !end_flag)
+                abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
-            if (s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
+            if (end_flag) break;
+            if (p.serve || s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
             float xl[KS];
             load_x<KS>(xl, xv, lane);
             float vn[CWK], out[CWK];
@@ -406,16 +455,20 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         Pref pf, pr;
         pref_issue(pr, edge(role - 2, t0) + c_lo, nres, tid);
         pref_issue(pf, edge(role - 1, t0), C, tid);
-        for (int s = 0; s < p.steps; ++s) {
+        for (int s = 0; p.serve || s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
             float* rv = rbuf + (s & 1) * kPipeMaxCh;
-            bool ok = pref_finish(pr, edge(role - 2, t) + c_lo, nres, (unsigned)t + 1u, rv, &abort_flag, p.fault, tid);
-            if (ok) ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid);
-            if (!ok) abort_flag = 1;
+            bool ok = pref_finish(pr, edge(role - 2, t) + c_lo, nres, (unsigned)t + 1u, rv, &abort_flag, p.fault, tid,
+                                  limit, endw, &end_flag);
+            if (ok)
+                ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, limit, endw,
+                                 &end_flag);
+            if (!ok && !end_flag) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
-            if (s + 1 < p.steps) {  // the next frame's loads are in flight during this one
+            if (end_flag) break;
+            if (p.serve || s + 1 < p.steps) {  // the next frame's loads are in flight during this one
                 pref_issue(pr, edge(role - 2, t + 1) + c_lo, nres, tid);
                 pref_issue(pf, edge(role - 1, t + 1), C, tid);
             }
@@ -439,8 +492,18 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 const int c = c_lo + wid + kWaves * lane;
                 if (is_p)
                     publish(out_edge(role, t) + c, (unsigned)t + 1u, y);
+                else if (p.serve)  // host-mapped pose ring
+                    __hip_atomic_store((unsigned*)p.poses + (int64_t)(t & (Q - 1)) * Nout + c, __float_as_uint(y),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 else
                     p.poses[(int64_t)(t & (Q - 1)) * Nout + c] = y;
+            }
+            if (p.serve && !is_p) {
+                // this workgroup's pose channels of frame t are in host memory: report it
+                __threadfence_system();
+                __syncthreads();
+                if (tid == 0)
+                    __hip_atomic_store(p.done_host + gi, (unsigned)t + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
     }
@@ -456,7 +519,9 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             if (l == nl) active = p.cu0[l];
         if (prev == (unsigned)active - 1u) {
             *p.arrivals = 0u;
-            __hip_atomic_store(p.frames_seen, t0 + p.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int t_end = p.serve ? (int)__hip_atomic_load(p.end_frame, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : t0 + p.steps;
+            __hip_atomic_store(p.frames_seen, t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -787,6 +788,14 @@ struct vp3d_stream {
     unsigned* err_host = nullptr;
     unsigned* err_host_dev = nullptr;
     unsigned long long spin_ticks = kStreamSpinTicks;
+    // serve form (pipe only): pinned host rings + control words, and the device end word
+    bool serving = false;
+    void* serve_host = nullptr;        // [ctrl: posted, stop, pad.., done[16]][frames Q x cin][poses Q x nout]
+    void* serve_dev = nullptr;         // device view of serve_host
+    unsigned* end_frame = nullptr;     // device word
+    int64_t posted = 0;                // host: frames posted so far (absolute)
+    int n_done = 0;                    // shrink workgroups reporting
+    hipStream_t serve_stream = nullptr;
 };
 
 namespace {
@@ -1130,6 +1139,7 @@ int vp3d_stream_status(vp3d_stream* st) {
 
 int vp3d_stream_reset(vp3d_stream* st, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (st->serving) return fail(VP3D_ERR_STATE, "serving: vp3d_stream_serve_end first");
     // position, arrival counter and the sticky timeout word; the host mirror is cleared
     // once no launch of this stream can still set it
     HIP_TRY(hipMemsetAsync(st->frames_seen, 0, 16, (hipStream_t)stream));
@@ -1151,6 +1161,7 @@ int vp3d_stream_io(vp3d_stream* st, float** in_frames, float** out_poses, int* q
 
 int vp3d_stream_step(vp3d_stream* st, const float* frame, float* pose, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (st->serving) return fail(VP3D_ERR_STATE, "serving: post frames with vp3d_stream_serve_post");
     if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
     hipStream_t s = (hipStream_t)stream;
     const int slot = (int)(st->host_t % kQueue);
@@ -1202,14 +1213,143 @@ int vp3d_stream_graph_capture(vp3d_stream* st, void* stream, int steps) {
 
 int vp3d_stream_graph_launch(vp3d_stream* st, void* stream) {
     if (!st || !st->exec) return fail(VP3D_ERR_STATE, "no captured graph");
+    if (st->serving) return fail(VP3D_ERR_STATE, "serving: post frames with vp3d_stream_serve_post");
     if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
     HIP_TRY(hipGraphLaunch(st->exec, (hipStream_t)stream));
     st->host_t += st->graph_steps;
     return VP3D_OK;
 }
 
+}  // extern "C"
+
+namespace {
+constexpr int kServeCtrlWords = 32;  // [0] posted, [1] stop, [2] ended (+1), [16 ..] done per shrink workgroup
+unsigned* serve_ctrl(vp3d_stream* st) { return (unsigned*)st->serve_host; }
+float* serve_frames(vp3d_stream* st) { return (float*)((char*)st->serve_host + kServeCtrlWords * 4); }
+float* serve_poses(vp3d_stream* st) {
+    return serve_frames(st) + (size_t)kQueue * st->h->layers[0].cin;
+}
+template <typename T>
+T* dev_view(vp3d_stream* st, T* host_ptr) {
+    return (T*)((char*)st->serve_dev + ((char*)host_ptr - (char*)st->serve_host));
+}
+unsigned serve_done_min(vp3d_stream* st) {
+    const volatile unsigned* done = serve_ctrl(st) + 16;
+    unsigned m = done[0];
+    for (int i = 1; i < st->n_done; ++i) m = std::min(m, (unsigned)done[i]);
+    return m;
+}
+}  // namespace
+
+extern "C" {
+
+int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (!st->pipe) return fail(VP3D_ERR_STATE, "serving needs the layer-pipelined form (vp3d_stream_mode 2)");
+    if (st->serving) return fail(VP3D_ERR_STATE, "already serving");
+    if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
+    if (!(idle_ms > 0.0) || idle_ms > 1000.0) return fail(VP3D_ERR_ARG, "idle_ms must be in (0, 1000]");
+    hipStream_t s = (hipStream_t)stream;
+    const vp3d_handle* h = st->h;
+    const int nl = (int)h->layers.size();
+    st->n_done = st->pipe_p.cu0[nl] - st->pipe_p.cu0[nl - 1];
+    if (st->n_done > 16) return fail(VP3D_ERR_STATE, "too many shrink workgroups to report");
+    if (!st->serve_host) {
+        const size_t bytes = kServeCtrlWords * 4 + (size_t)kQueue * (h->layers[0].cin + h->layers.back().cout) * 4;
+        HIP_TRY(hipHostMalloc(&st->serve_host, bytes, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer(&st->serve_dev, st->serve_host, 0));
+        HIP_TRY(hipMalloc(&st->end_frame, 4));
+    }
+    // the stream position of the device (any earlier launches on `stream` finished)
+    HIP_TRY(hipStreamSynchronize(s));
+    int pos = 0;
+    HIP_TRY(hipMemcpy(&pos, st->frames_seen, 4, hipMemcpyDeviceToHost));
+    st->host_t = pos;
+    st->posted = pos;
+    volatile unsigned* ctrl = serve_ctrl(st);
+    ctrl[0] = (unsigned)pos;
+    ctrl[1] = 0u;
+    ctrl[2] = 0u;
+    for (int i = 0; i < 16; ++i) ctrl[16 + i] = (unsigned)pos;
+    HIP_TRY(hipMemsetAsync(st->end_frame, 0xff, 4, s));
+    StreamPipeParams p = st->pipe_p;
+    p.serve = 1;
+    p.frames = dev_view(st, serve_frames(st));
+    p.poses = dev_view(st, serve_poses(st));
+    p.posted = dev_view(st, serve_ctrl(st));
+    p.stop = dev_view(st, serve_ctrl(st) + 1);
+    p.done_host = dev_view(st, serve_ctrl(st) + 16);
+    p.ended_host = dev_view(st, serve_ctrl(st) + 2);
+    p.end_frame = st->end_frame;
+    p.idle_ticks = (unsigned long long)(idle_ms * 1e5);  // 100 MHz clock
+    p.steps = 0;
+    const Act wt = st->dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16;
+    HIP_TRY(launch_stream_pipe(p, wt, st->pipe_lds, s));
+    st->serving = true;
+    st->serve_stream = s;
+    return VP3D_OK;
+}
+
+int vp3d_stream_serve_post(vp3d_stream* st, const float* frame, int64_t* frame_index) {
+    if (!st || !frame) return fail(VP3D_ERR_ARG, "NULL argument");
+    if (!st->serving) return fail(VP3D_ERR_STATE, "not serving (vp3d_stream_serve_begin)");
+    if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
+    if (((volatile unsigned*)serve_ctrl(st))[2]) return fail(VP3D_ERR_STATE, "the serve launch ended (idle); vp3d_stream_serve_end, then begin");
+    if (st->posted - (int64_t)serve_done_min(st) >= kQueue - 1)
+        return fail(VP3D_ERR_STATE, "serve ring full: wait for earlier frames first");
+    const int cin = st->h->layers[0].cin;
+    const int64_t t = st->posted;
+    std::memcpy(serve_frames(st) + (size_t)(t % kQueue) * cin, frame, 4 * (size_t)cin);
+    // the frame's bytes before the count (x86 stores are ordered; the release keeps the
+    // compiler from reordering them)
+    __atomic_store_n(serve_ctrl(st), (unsigned)(t + 1), __ATOMIC_RELEASE);
+    st->posted = t + 1;
+    if (frame_index) *frame_index = t;
+    return VP3D_OK;
+}
+
+int vp3d_stream_serve_wait(vp3d_stream* st, int64_t frame_index, float* pose, double timeout_ms) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (!st->serving) return fail(VP3D_ERR_STATE, "not serving (vp3d_stream_serve_begin)");
+    if (frame_index < 0 || frame_index >= st->posted) return fail(VP3D_ERR_ARG, "frame was not posted");
+    if (st->posted - frame_index >= kQueue) return fail(VP3D_ERR_ARG, "frame's pose slot was reused");
+    const volatile unsigned* done = serve_ctrl(st) + 16;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        bool all = true;
+        for (int i = 0; i < st->n_done; ++i)
+            if ((int64_t)done[i] <= frame_index) all = false;
+        if (all) break;
+        if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
+        const unsigned ended = ((volatile unsigned*)serve_ctrl(st))[2];
+        if (ended && (int64_t)ended - 1 <= frame_index) return fail(VP3D_ERR_STATE, "the serve launch ended before this frame");
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > timeout_ms) return fail(VP3D_ERR_STATE, "serve wait timed out (the launch ended or is stalled)");
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const int nout = st->h->layers.back().cout;
+    if (pose) std::memcpy(pose, serve_poses(st) + (size_t)(frame_index % kQueue) * nout, 4 * (size_t)nout);
+    return VP3D_OK;
+}
+
+int vp3d_stream_serve_end(vp3d_stream* st, void* stream) {
+    if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
+    if (!st->serving) return VP3D_OK;
+    __atomic_store_n(serve_ctrl(st) + 1, 1u, __ATOMIC_RELEASE);
+    st->serving = false;
+    HIP_TRY(hipStreamSynchronize(stream ? (hipStream_t)stream : st->serve_stream));
+    int pos = 0;
+    HIP_TRY(hipMemcpy(&pos, st->frames_seen, 4, hipMemcpyDeviceToHost));
+    st->host_t = pos;
+    if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
+    return VP3D_OK;
+}
+
 int vp3d_stream_destroy(vp3d_stream* st) {
     if (!st) return VP3D_OK;
+    if (st->serving) vp3d_stream_serve_end(st, nullptr);
+    hipHostFree(st->serve_host);
+    hipFree(st->end_frame);
     if (st->exec) hipGraphExecDestroy(st->exec);
     if (st->graph) hipGraphDestroy(st->graph);
     hipFree(st->frames_seen);

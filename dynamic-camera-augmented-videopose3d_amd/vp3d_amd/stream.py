@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _native as N
@@ -72,6 +73,15 @@ class CausalStream:
         with torch.cuda.device(self.device):
             N.check(self._lib.vp3d_stream_status(self._s), "vp3d_stream_status")
 
+    # ---- serving: the pipelined launch stays resident, frames posted from the host ----
+    def serve(self, idle_ms: float = 200.0, stream: torch.cuda.Stream | None = None) -> "Serving":
+        """Context manager for real-time use, one frame in flight (config 5's single-frame
+        latency): the layer-pipelined launch (mode 'pipe') stays resident with its weights
+        in VGPRs; `post(frame)` writes a host frame into pinned memory, `wait(t)` spins on
+        pinned memory until pose t is there -- no launch, copy or graph per frame.  The
+        launch ends itself after `idle_ms` without a frame."""
+        return Serving(self, idle_ms, stream)
+
     # ---- hipGraph replay: steps read the device frame queue, write the pose ring ----
     def io_tensors(self):
         """(frame_queue (Q, J_in*F), pose_ring (Q, J_out*3)) views of the device buffers:
@@ -102,6 +112,45 @@ class CausalStream:
             self.close()
         except Exception:
             pass
+
+
+class Serving:
+    """A resident serve launch of a CausalStream (vp3d_stream_serve_*)."""
+
+    def __init__(self, st: CausalStream, idle_ms: float, stream):
+        self.st, self.idle_ms = st, float(idle_ms)
+        self.stream = stream if stream is not None else torch.cuda.Stream(st.device)
+        self._pose = np.empty(st.n_out, dtype=np.float32)
+
+    def __enter__(self):
+        with torch.cuda.device(self.st.device):
+            N.check(self.st._lib.vp3d_stream_serve_begin(self.st._s, self.stream.cuda_stream, self.idle_ms),
+                    "vp3d_stream_serve_begin")
+        return self
+
+    def post(self, frame) -> int:
+        """Post one frame ((J_in, F) host float32); returns its stream index."""
+        f = np.ascontiguousarray(np.asarray(frame, dtype=np.float32)).reshape(-1)
+        assert f.size == self.st.n_in
+        t = ctypes.c_int64()
+        N.check(self.st._lib.vp3d_stream_serve_post(self.st._s, f.ctypes.data, ctypes.byref(t)),
+                "vp3d_stream_serve_post")
+        return int(t.value)
+
+    def wait(self, t: int, timeout_ms: float = 1000.0) -> np.ndarray:
+        """Pose (J_out, 3) of frame t (host float32)."""
+        out = np.empty(self.st.n_out, dtype=np.float32)
+        N.check(self.st._lib.vp3d_stream_serve_wait(self.st._s, int(t), out.ctypes.data, float(timeout_ms)),
+                "vp3d_stream_serve_wait")
+        return out.reshape(-1, 3)
+
+    def step(self, frame) -> np.ndarray:
+        return self.wait(self.post(frame))
+
+    def __exit__(self, *exc):
+        with torch.cuda.device(self.st.device):
+            N.check(self.st._lib.vp3d_stream_serve_end(self.st._s, self.stream.cuda_stream), "vp3d_stream_serve_end")
+        return False
 
 
 class _DevBuf:

@@ -191,6 +191,23 @@ int vp3d_stream_mode(const vp3d_stream* s);
  * (bounded spins: the grid did not fit the device at once), else VP3D_OK. */
 int vp3d_stream_status(vp3d_stream* s);
 
+/* ---- serving: one frame in flight, real time (config 5's single-frame latency) ----
+ * The layer-pipelined launch (mode 2) stays resident with its weights in VGPRs and takes
+ * frames as the host posts them through pinned host memory; the pose of frame t comes back
+ * the same way, with no launch, copy or graph per frame.  The launch ends by itself at
+ * the first frame not posted within idle_ms, or at vp3d_stream_serve_end.  Frames keep
+ * the stream's numbering (the first posted frame is frame vp3d_stream_frames_seen()).
+ * At most queue_len - 1 frames may be posted and not yet waited for. */
+int vp3d_stream_serve_begin(vp3d_stream* s, void* stream, double idle_ms);
+/* Copy one frame (host f32, J_in * F values) into the ring and post it; *frame_index is
+ * its stream index.  VP3D_ERR_STATE when not serving, the ring is full or the launch ended. */
+int vp3d_stream_serve_post(vp3d_stream* s, const float* frame, int64_t* frame_index);
+/* Wait (spinning on host memory, at most timeout_ms) until frame `frame_index` is done and
+ * copy its pose (host f32, J_out * 3) out.  VP3D_ERR_STATE on timeout or stream fault. */
+int vp3d_stream_serve_wait(vp3d_stream* s, int64_t frame_index, float* pose, double timeout_ms);
+/* Stop serving: the launch finishes the posted frames and exits; synchronises `stream`. */
+int vp3d_stream_serve_end(vp3d_stream* s, void* stream);
+
 /* ---- training step (run.py:451-487, :662) ----
  * The reference trains TemporalModel in train mode: BatchNorm1d on batch
  * statistics with a running-stat update (TemporalModel.py:117,119; momentum

@@ -145,3 +145,42 @@ def test_stream_timeout_is_sticky(mode, monkeypatch):
     st.reset()
     st.check()
     assert st.frames_seen() == 0
+
+
+def test_stream_serve_one_frame_in_flight():
+    """Serving (vp3d_stream_serve_*): the pipelined launch stays resident and takes frames
+    posted from host memory one at a time.  Poses equal the whole-sequence causal
+    reference (fp16 gate) and, bit for bit, the batch form's; frames may be posted ahead;
+    the stream continues seamlessly in the batch form after serving; an idle launch ends
+    itself and further posts are refused."""
+    import time
+    fw = (3, 3, 3, 3, 3)
+    m, sd = make_model(False, fw, causal=True)
+    T = 96
+    x = synth.normalized_windows(19, "stream_serve", 1, T)
+    ref = _ref(sd, x, fw)
+    m.cuda()
+    st = CausalStream(m.native_lifter(), "fp16")
+    assert st.mode == "pipe"
+    with st.serve(idle_ms=500.0) as sv:
+        served = [sv.step(x[0, t]) for t in range(48)]
+        ts = [sv.post(x[0, t]) for t in range(48, 64)]  # 16 frames in flight at once
+        assert ts == list(range(48, 64))
+        served += [sv.wait(t) for t in ts]
+    assert st.frames_seen() == 64
+    xs = torch.from_numpy(x[0]).cuda()
+    rest = [st.step(xs[t]).cpu().numpy() for t in range(64, T)]  # batch form continues
+    out = np.concatenate([np.stack(served), np.stack(rest)])
+    err = np.abs(out - ref).max()
+    print(f"serve fp16: max|d|={err:.3e} m")
+    assert err <= 3e-4
+    st.reset()
+    batch = torch.stack([st.step(xs[t]).clone() for t in range(64)]).cpu().numpy()
+    np.testing.assert_array_equal(np.stack(served), batch)
+    # an idle launch ends itself; the next post is refused until serving restarts
+    with st.serve(idle_ms=5.0) as sv:
+        sv.step(x[0, 64])
+        time.sleep(0.05)
+        with pytest.raises(RuntimeError, match="ended"):
+            sv.post(x[0, 65])
+    assert st.frames_seen() == 65
