@@ -77,27 +77,28 @@ __device__ __forceinline__ void exp_vm() {
 // and lo halves, each 32-wide K group [hi(32) | lo(32)], BN NOT folded), so a weight chunk
 // is 2 NKS slabs (hi, lo per k-slab) and each k-slab issues hi.hi + hi.lo + lo.hi; the
 // epilogue applies the BatchNorm as ATen does (x * scale, then + shift, two roundings) +
-// ReLU and writes the split output row (channel n at 64 (n / 32) + n % 32, lo 32 further):
-// 256 output bytes per row per 64-channel chunk, staged per wave and stored as 16-byte
-// pieces, 4 rows x 256 B per instruction.  One workgroup per CU (LDS), 4 waves.
+// ReLU in the accumulator layout, then (as gemm::epilogue_tp) one v_permlane16_swap per
+// value pair gives each lane 8 consecutive channels of a row, stored straight from
+// registers as 16 bytes of hi and 16 of lo (channel n at 64 (n / 32) + n % 32 of the split
+// row, lo 32 further): no LDS staging, so with a 2-chunk weight ring two workgroups share
+// a CU and one's epilogue runs under the other's MFMAs.
 template <typename CT, int NKS, int RB, bool GATHER, bool NT = false, int RING = 3, bool X3 = false>
-__global__ __launch_bounds__(256, X3 ? 1 : 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
+__global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
     constexpr int kRowsW = 16 * RB;
     constexpr int kRows = kRowsW * kExpWaves;
     constexpr int NKW = X3 ? 2 * NKS : NKS;  // weight slabs per chunk
     constexpr int kChunk = NKW * kExpSlab;
-    constexpr int kRowB = X3 ? 256 : 128;  // staged output bytes per row and chunk
-    // ring of weight chunks, then per-wave output staging: kRowsW rows x kRowB, 16-byte
-    // unit c of row r at c ^ (r & 7) (X3: c ^ (r & 15)); X3: then scale, shift (N floats each)
-    __shared__ __attribute__((aligned(16))) char smem[RING * kChunk + kExpWaves * kRowsW * kRowB +
-                                                      (X3 ? 2 * kExpMaxN * 4 : 0)];
+    // ring of weight chunks, then (16-bit) per-wave output staging: kRowsW rows x 128 B,
+    // 16-byte unit c of row r at c ^ (r & 7); X3: scale, shift (N floats each) instead
+    __shared__ __attribute__((aligned(16))) char smem[RING * kChunk +
+                                                      (X3 ? 2 * kExpMaxN * 4 : kExpWaves * kRowsW * 128)];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int m_wave = blockIdx.x * kRows + wid * kRowsW;
-    u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * kRowB);
-    float* const s_scale = (float*)(smem + RING * kChunk + kExpWaves * kRowsW * kRowB);
+    u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * 128);
+    float* const s_scale = (float*)(smem + RING * kChunk);
     float* const s_shift = s_scale + kExpMaxN;
     if constexpr (X3) {
         for (int i = tid; i < p.N; i += 256) {
@@ -273,46 +274,57 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void expand_gemm_h16(ConvGemmParam
 #pragma unroll
                     for (int j = 0; j < 4; ++j) acc[rb][j] = mfma16<CT>(wl[j], af[rb][ks], acc[rb][j]);
             }
-            // epilogue: BN affine (two roundings) + ReLU, split into hi / lo, staged per row
+            // epilogue: BN affine (two roundings) + ReLU in the accumulator layout (lane: channels
+            // n0 + 16 j + 4 (l >> 4) + r of row 16 rb + (l & 15)); the permlane swap pairs j = 2 jp,
+            // 2 jp + 1 so each lane then holds channels n0 + 32 jp + c0 + 0..7 of its row
             const int n0 = ch * kExpChunkN;
+            const int grp = lane >> 4;
+            const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+            float sc[4][4], sh[4][4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int nl = j * 16 + (lane >> 4) * 4;
-                const f32x4 sc = *(const f32x4*)&s_scale[n0 + nl];
-                const f32x4 sh = *(const f32x4*)&s_shift[n0 + nl];
-                const int uh = (nl >> 5) * 8 + ((nl & 31) >> 3);
-                const int half = (nl >> 2) & 1;
+                const f32x4 s4 = *(const f32x4*)&s_scale[n0 + 16 * j + 4 * grp];
+                const f32x4 h4 = *(const f32x4*)&s_shift[n0 + 16 * j + 4 * grp];
 #pragma unroll
-                for (int rb = 0; rb < RB; ++rb) {
-                    f16 h[4], l[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = __fadd_rn(__fmul_rn(acc[rb][j][r], sc[r]), sh[r]);
-                        if (p.relu) v = v > 0.f ? v : 0.f;
-                        h[r] = (f16)v;
-                        l[r] = (f16)(v - (float)h[r]);
-                    }
-                    const int row = rb * 16 + (lane & 15);
-                    char* base = (char*)stage + row * 256 + (half << 3);
-                    typedef f16 f16x4 __attribute__((ext_vector_type(4)));
-                    *(f16x4*)(base + ((uh ^ (row & 15)) << 4)) = f16x4{h[0], h[1], h[2], h[3]};
-                    *(f16x4*)(base + (((uh + 4) ^ (row & 15)) << 4)) = f16x4{l[0], l[1], l[2], l[3]};
+                for (int r = 0; r < 4; ++r) {
+                    sc[j][r] = s4[r];
+                    sh[j][r] = h4[r];
                 }
             }
-            asm volatile("" ::: "memory");
-            // 16 lanes per row, 4 rows per instruction: 256 B of a row (2 whole lines)
 #pragma unroll
-            for (int q = 0; q < 4 * RB; ++q) {
-                const int row = q * 4 + (lane >> 4);
-                const int c16 = lane & 15;
-                const u32x4 v = stage[row * 16 + (c16 ^ (row & 15))];
-                const int m = m_wave + row;
-                if (m < p.M) {
-                    u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + c16 * 8);
-                    if constexpr (NT)
-                        __builtin_nontemporal_store(v, dst);
-                    else
-                        *dst = v;
+            for (int rb = 0; rb < RB; ++rb) {
+                const int m = m_wave + rb * 16 + (lane & 15);
+#pragma unroll
+                for (int jp = 0; jp < 2; ++jp) {
+                    float v[8];
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        float x = __fadd_rn(__fmul_rn(acc[rb][2 * jp][d], sc[2 * jp][d]), sh[2 * jp][d]);
+                        float y = __fadd_rn(__fmul_rn(acc[rb][2 * jp + 1][d], sc[2 * jp + 1][d]), sh[2 * jp + 1][d]);
+                        if (p.relu) {
+                            x = x > 0.f ? x : 0.f;
+                            y = y > 0.f ? y : 0.f;
+                        }
+                        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+                        v[d] = x;
+                        v[d + 4] = y;
+                    }
+                    f16x8 oh, ol;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        oh[e] = (f16)v[e];
+                        ol[e] = (f16)(v[e] - (float)oh[e]);
+                    }
+                    if (m < p.M) {
+                        u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + 64 * jp + c0);
+                        if constexpr (NT) {
+                            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, oh), dst);
+                            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, ol), dst + 4);
+                        } else {
+                            dst[0] = __builtin_bit_cast(u32x4, oh);
+                            dst[4] = __builtin_bit_cast(u32x4, ol);
+                        }
+                    }
                 }
             }
             asm volatile("" ::: "memory");
@@ -322,7 +334,7 @@ __global__ __launch_bounds__(256, X3 ? 1 : 2) void expand_gemm_h16(ConvGemmParam
                 else if (RING == 3 && ch + 2 < nchunks)
                     exp_vm<NKW + 4 * RB>();
                 else
-                    exp_vm<4 * RB>();
+                    exp_vm<4 * RB>();  // this chunk's stores: RB row blocks x 2 channel halves x (hi, lo)
             }
             __builtin_amdgcn_s_barrier();
             continue;
@@ -496,11 +508,13 @@ hipError_t launch_expand_gemm_x3(const ConvGemmParams& p, const GatherSrc* g, hi
     const int nks = (p.K + 31) / 32;
     const bool nt = (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
     const GatherSrc none{};
+    // RB 2 row blocks per wave, 2-chunk weight ring: 2 x 32 KB + 8 KB scale / shift (NKS 4),
+    // two workgroups per CU
     if (g)
-        return nt ? launch_rb_nt<f16, 2, true, true, 3, true>(p, *g, nks, stream)
-                  : launch_rb_nt<f16, 2, true, false, 3, true>(p, *g, nks, stream);
-    return nt ? launch_rb_nt<f16, 2, false, true, 3, true>(p, none, nks, stream)
-              : launch_rb_nt<f16, 2, false, false, 3, true>(p, none, nks, stream);
+        return nt ? launch_rb_nt<f16, 2, true, true, 2, true>(p, *g, nks, stream)
+                  : launch_rb_nt<f16, 2, true, false, 2, true>(p, *g, nks, stream);
+    return nt ? launch_rb_nt<f16, 2, false, true, 2, true>(p, none, nks, stream)
+              : launch_rb_nt<f16, 2, false, false, 2, true>(p, none, nks, stream);
 }
 
 }  // namespace vp3d
