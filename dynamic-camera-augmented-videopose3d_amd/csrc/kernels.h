@@ -53,6 +53,8 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
 // 64-deep K-tiles staged as whole 128-byte lines, quadrant phases (conv_gemm_q64.hip).
 bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream);
+// One wave per SIMD, 128 x 128 wave tiles (conv_gemm_q4w.hip); q64's contract.
+hipError_t launch_conv_gemm_q4w(const ConvGemmParams& p, Act compute, hipStream_t stream);
 // Split-fp16 mode of conv_gemm_q64 (VP3D_DTYPE_F16X3): A / W / residual rows of f16 halves,
 // each 32-wide K group [hi(32) | lo(32)] (Ktap, Kp, lda, ldr in halves); output split
 // (ldy halves) or, out_f32, f32 rows (ldy floats).  N % 64 == 0, N <= 1024.
@@ -196,6 +198,11 @@ struct StreamPipeParams {
     unsigned* done_host;
     unsigned* ended_host;                  // host-mapped copy of the end frame + 1 (0 while serving)
     unsigned long long idle_ticks;
+    // diagnostics (VP3D_STREAM_TRACE=n at vp3d_stream_create): thread 0 of every workgroup
+    // records the 100 MHz clock when the input of its frame s < trace_frames is complete and
+    // after its first output store: trace[(wg * trace_frames + s) * 2 + {0, 1}]
+    unsigned long long* trace;
+    int trace_frames;
 };
 int stream_pipe_lds_bytes(int C, int cin0, int max_ring);
 bool stream_pipe_channels_ok(int C);

@@ -196,6 +196,11 @@ __device__ __forceinline__ float lane_select(const float (&v)[CW]) {
     return __builtin_bit_cast(float, r);
 }
 
+__device__ __forceinline__ void trace_mark(const StreamPipeParams& p, int wg, int s, int k, int tid) {
+    if (p.trace && tid == 0 && s < p.trace_frames)
+        p.trace[((int64_t)wg * p.trace_frames + s) * 2 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 }  // namespace
 
 template <typename WT, int KS>
@@ -319,6 +324,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 __syncthreads();
                 if (end_flag) break;
             }
+            trace_mark(p, wg, s, 0, tid);
             float* xv = xin + (s & 1) * kPipeExpandK;
             const float* fr = p.frames + (int64_t)(t & (Q - 1)) * cin0;
             for (int i = tid; i < cin0; i += kThreads) {
@@ -348,6 +354,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 y = y > 0.f ? y : 0.f;
                 publish(out_edge(0, t) + c, (unsigned)t + 1u, y);
             }
+            trace_mark(p, wg, s, 1, tid);
             // the next frame writes the other xin buffer; hist is rewritten only after the
             // next barrier, which every wave passes after its reads of this frame
         }
@@ -378,6 +385,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             __syncthreads();
             if (abort_flag) return;
             if (end_flag) break;
+            trace_mark(p, wg, s, 0, tid);
             if (p.serve || s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
             float xl[KS];
             load_x<KS>(xl, xv, lane);
@@ -402,6 +410,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 }
                 if (lane < nown)
                     publish(out_edge(role, t) + c_lo + wid + kWaves * lane, (unsigned)t + 1u, lane_select<CWK>(out));
+                trace_mark(p, wg, s, 1, tid);
                 // ring: all slots zero, then outputs tt = 1..2d from the clamped taps
                 for (int i = lane; i < R * CWK; i += 64) wring[i] = 0.f;
                 if (lane < CWK) {
@@ -420,6 +429,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 }
                 if (lane < nown)
                     publish(out_edge(role, t) + c_lo + wid + kWaves * lane, (unsigned)t + 1u, lane_select<CWK>(out));
+                trace_mark(p, wg, s, 1, tid);
                 // the older taps of x(t) feed outputs t + d (tap 1) and t + 2d (tap 0)
                 float v0[CWK], v1[CWK];
                 lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1);
@@ -468,6 +478,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             __syncthreads();
             if (abort_flag) return;
             if (end_flag) break;
+            trace_mark(p, wg, s, 0, tid);
             if (p.serve || s + 1 < p.steps) {  // the next frame's loads are in flight during this one
                 pref_issue(pr, edge(role - 2, t + 1) + c_lo, nres, tid);
                 pref_issue(pf, edge(role - 1, t + 1), C, tid);
@@ -505,6 +516,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 if (tid == 0)
                     __hip_atomic_store(p.done_host + gi, (unsigned)t + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
+            trace_mark(p, wg, s, 1, tid);
         }
     }
     // ---- the last workgroup to finish advances the stream position (every workgroup read

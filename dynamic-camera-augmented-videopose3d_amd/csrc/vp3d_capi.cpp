@@ -782,6 +782,7 @@ struct vp3d_stream {
     int pipe_lds = 0;
     unsigned long long* pipe_gran = nullptr;  // [queue][2nb+1][C] granules, cleared at reset
     size_t pipe_gran_bytes = 0;
+    unsigned long long* pipe_trace = nullptr;  // VP3D_STREAM_TRACE diagnostics
     float* pipe_state = nullptr;
     // persistent forms: host-mapped mirror of the sticky timeout word (frames_seen[3]), read
     // by step / graph_launch without a synchronisation
@@ -990,6 +991,14 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     p.fault = StreamFault{(unsigned*)(st->frames_seen + 3), st->err_host_dev, st->spin_ticks};
     p.gran = st->pipe_gran;
     p.state = st->pipe_state;
+    if (const char* e = getenv("VP3D_STREAM_TRACE")) {
+        const int n = atoi(e);
+        if (n > 0 && hipMalloc(&st->pipe_trace, (size_t)g * n * 16) == hipSuccess) {
+            hipMemset(st->pipe_trace, 0, (size_t)g * n * 16);
+            p.trace = st->pipe_trace;
+            p.trace_frames = n;
+        }
+    }
     return true;
 }
 
@@ -1345,6 +1354,24 @@ int vp3d_stream_serve_end(vp3d_stream* st, void* stream) {
     return VP3D_OK;
 }
 
+int vp3d_stream_trace(vp3d_stream* st, uint64_t* out, int64_t capacity, int32_t* role_first_wg, int32_t* n_roles,
+                      int32_t* frames) {
+    if (!st || !n_roles || !frames) return fail(VP3D_ERR_ARG, "NULL argument");
+    if (!st->pipe_trace) return fail(VP3D_ERR_STATE, "no trace: set VP3D_STREAM_TRACE=n before vp3d_stream_create");
+    const StreamPipeParams& p = st->pipe_p;
+    *n_roles = p.nl;
+    *frames = p.trace_frames;
+    if (role_first_wg)
+        for (int l = 0; l <= p.nl; ++l) role_first_wg[l] = p.cu0[l];
+    const int64_t need = (int64_t)p.cu0[p.nl] * p.trace_frames * 2;
+    if (!out) return VP3D_OK;
+    if (capacity < need) return fail(VP3D_ERR_ARG, "trace buffer too small");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, st->pipe_trace, (size_t)need * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(st->pipe_trace, 0, (size_t)need * 8));
+    return VP3D_OK;
+}
+
 int vp3d_stream_destroy(vp3d_stream* st) {
     if (!st) return VP3D_OK;
     if (st->serving) vp3d_stream_serve_end(st, nullptr);
@@ -1361,6 +1388,7 @@ int vp3d_stream_destroy(vp3d_stream* st) {
     hipFree(st->pstate);
     hipFree(st->pipe_gran);
     hipFree(st->pipe_state);
+    hipFree(st->pipe_trace);
     hipHostFree(st->err_host);
     delete st;
     return VP3D_OK;

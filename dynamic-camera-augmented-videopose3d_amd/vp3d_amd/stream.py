@@ -82,6 +82,23 @@ class CausalStream:
         launch ends itself after `idle_ms` without a frame."""
         return Serving(self, idle_ms, stream)
 
+    def trace(self):
+        """Per-frame device clocks of the layer-pipelined launch (VP3D_STREAM_TRACE=n set
+        before the stream was created): returns (clocks, role_first_wg) with clocks of shape
+        (workgroups, n, 2) -- [..., 0] input complete, [..., 1] first output stored, 100 MHz
+        ticks, 0 = not recorded -- for the first n frames of the last launch, then clears them."""
+        roles, frames = ctypes.c_int32(), ctypes.c_int32()
+        N.check(self._lib.vp3d_stream_trace(self._s, None, 0, None, ctypes.byref(roles), ctypes.byref(frames)),
+                "vp3d_stream_trace")
+        first = np.zeros(roles.value + 1, np.int32)
+        N.check(self._lib.vp3d_stream_trace(self._s, None, 0, first.ctypes.data, ctypes.byref(roles),
+                                            ctypes.byref(frames)), "vp3d_stream_trace")
+        out = np.zeros((int(first[-1]), frames.value, 2), np.uint64)
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_stream_trace(self._s, out.ctypes.data, out.size, first.ctypes.data,
+                                                ctypes.byref(roles), ctypes.byref(frames)), "vp3d_stream_trace")
+        return out, first
+
     # ---- hipGraph replay: steps read the device frame queue, write the pose ring ----
     def io_tensors(self):
         """(frame_queue (Q, J_in*F), pose_ring (Q, J_out*3)) views of the device buffers:

@@ -207,6 +207,14 @@ int vp3d_stream_serve_post(vp3d_stream* s, const float* frame, int64_t* frame_in
 int vp3d_stream_serve_wait(vp3d_stream* s, int64_t frame_index, float* pose, double timeout_ms);
 /* Stop serving: the launch finishes the posted frames and exits; synchronises `stream`. */
 int vp3d_stream_serve_end(vp3d_stream* s, void* stream);
+/* Diagnostics of the layer-pipelined form (no reference counterpart): with VP3D_STREAM_TRACE=n
+ * set at vp3d_stream_create, every workgroup records the 100 MHz device clock when the input of
+ * each of the first n frames of a launch is complete and after its first output store.  Copies
+ * workgroups x n x 2 clocks to `out` (NULL: sizes only) and clears them; role_first_wg (n_roles
+ * + 1 entries, or NULL) = the first workgroup of each layer role (expand, k / 1x1 per block,
+ * shrink).  Synchronises the device. */
+int vp3d_stream_trace(vp3d_stream* s, uint64_t* out, int64_t capacity, int32_t* role_first_wg, int32_t* n_roles,
+                      int32_t* frames);
 
 /* ---- training step (run.py:451-487, :662) ----
  * The reference trains TemporalModel in train mode: BatchNorm1d on batch
