@@ -53,8 +53,6 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
 // 64-deep K-tiles staged as whole 128-byte lines, quadrant phases (conv_gemm_q64.hip).
 bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream);
-// One wave per SIMD, 128 x 128 wave tiles (conv_gemm_q4w.hip); q64's contract.
-hipError_t launch_conv_gemm_q4w(const ConvGemmParams& p, Act compute, hipStream_t stream);
 // Split-fp16 mode of conv_gemm_q64 (VP3D_DTYPE_F16X3): A / W / residual rows of f16 halves,
 // each 32-wide K group [hi(32) | lo(32)] (Ktap, Kp, lda, ldr in halves); output split
 // (ldy halves) or, out_f32, f32 rows (ldy floats).  N % 64 == 0, N <= 1024.
@@ -186,16 +184,18 @@ struct StreamPipeParams {
     int state_stride;
     int steps;
     // serve form (vp3d_stream_serve_*): the launch stays resident and takes frames as the
-    // host posts them -- `frames` / `poses` are then host-mapped rings, frame t is readable
-    // once *posted > t, and the shrink workgroups report frame t done by done_host[i] = t + 1
-    // (i = shrink workgroup).  The expand role ends the launch at the first frame not posted
-    // within idle_ticks (100 MHz clock) or once *stop is set, by writing it to *end_frame
-    // (device word, all ones while serving); every other role leaves when it reaches that frame.
+    // host posts them.  Frames and poses travel as 8-byte {tag = frame + 1, f32 value}
+    // granules in host-mapped rings (queue slots of cin0 / N[nl-1] granules): the expand role
+    // polls the frame granules themselves (no separate count to read first) and the shrink
+    // role stores pose granules the host polls (no fence or done word after them).  The
+    // expand role ends the launch at the first frame not posted within idle_ticks (100 MHz
+    // clock) or once *stop is set, by writing it to *end_frame (device word, all ones while
+    // serving); every other role leaves when it reaches that frame.
     int serve;
-    const unsigned* posted;
+    const unsigned long long* frame_gran;
+    unsigned long long* pose_gran;
     const unsigned* stop;
     unsigned* end_frame;
-    unsigned* done_host;
     unsigned* ended_host;                  // host-mapped copy of the end frame + 1 (0 while serving)
     unsigned long long idle_ticks;
     // diagnostics (VP3D_STREAM_TRACE=n at vp3d_stream_create): thread 0 of every workgroup

@@ -57,18 +57,49 @@ __device__ __forceinline__ float hi16(uint32_t w) {
     return (float)__builtin_bit_cast(WT, (unsigned short)(w >> 16));
 }
 
-// Sum over the 64 lanes, wave-uniform result.  Within each 16-lane row: xor 1, xor 2
-// (quad_perm), half-mirror, mirror; then the four row sums in a fixed order.
-__device__ __forceinline__ float wave_sum_uniform(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
-    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
-    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
-    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
-    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
-    return (r0 + r1) + (r2 + r3);
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// Lane-partial sums of CW <= 8 rows -> row totals, as a reduce-scatter over the wave: each
+// exchange step halves the rows a lane still carries (v_permlane32_swap: lanes 0-31 keep the
+// first half of the rows, 32-63 the second; v_permlane16_swap: the same between even and
+// odd 16-lane rows; for 8 rows a DPP rotate by 8 inside the 16-lane row), then the lanes that
+// share a row add up (DPP xor 1, xor 2, half mirror[, mirror]).  Lane l returns the total of
+// row l >> 3 (CW > 4) or l >> 4 (CW <= 4; rows past CW are zero).  About 18 instructions for
+// 8 rows instead of 8 full-wave reductions and the moves that put row j's sum into lane j.
+template <int CW>
+__device__ __forceinline__ float rows_sum(const float (&v)[CW], int lane) {
+    constexpr int P = CW <= 4 ? 4 : 8;
+    float s[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) s[j] = j < CW ? v[j] : 0.f;
+#pragma unroll
+    for (int k = 0; k < P / 2; ++k) {
+        float x = s[k], y = s[k + P / 2];
+        // x, y were just written by VALU -> 2 wait states (inline asm: see gemm_common.h)
+        asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+        s[k] = x + y;  // lanes 0-31: row k, lanes 32-63: row k + P/2
+    }
+#pragma unroll
+    for (int k = 0; k < P / 4; ++k) {
+        float x = s[k], y = s[k + P / 4];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+        s[k] = x + y;  // even 16-lane rows: row k (+ P/2), odd: row k + P/4 (+ P/2)
+    }
+    float r;
+    if constexpr (P == 8) {
+        const float a = s[0] + dpp<0x128>(s[0]), b = s[1] + dpp<0x128>(s[1]);  // row_ror:8 = xor 8
+        r = (lane & 8) ? b : a;
+    } else {
+        r = s[0];
+    }
+    r += dpp<0xB1>(r);   // xor 1
+    r += dpp<0x4E>(r);   // xor 2
+    r += dpp<0x141>(r);  // half mirror: the other quad of the 8 lanes
+    if constexpr (P == 4) r += dpp<0x140>(r);  // mirror: the other 8 lanes of the 16
+    return r;
 }
 
 __device__ __forceinline__ void publish(gu64* g, unsigned tag, float v) {
@@ -80,6 +111,8 @@ __device__ __forceinline__ void publish(gu64* g, unsigned tag, float v) {
 // current frame computes: pref_issue loads this thread's granules (tid, tid + kThreads of
 // an edge slice of n <= 2 * kThreads), pref_finish checks their tags, re-polls the ones
 // still missing (bounded, as sweep) and stores the values into x (LDS).
+constexpr unsigned long long kEndCheckTicks = 1000;  // 10 us of the 100 MHz clock
+
 struct Pref {
     unsigned long long v[2];
 };
@@ -92,7 +125,20 @@ __device__ __forceinline__ void pref_issue(Pref& r, const gu64* g, int n, int ti
 
 // true once every granule carried `tag`; false on timeout (sets the fault words) or when
 // another wave aborted, or -- serve form -- once the launch ended before frame tag - 1
-// (*end < tag: that frame is never produced; *ended is then set)
+// (*end < tag: that frame is never produced; *ended is then set).
+// Two poll rounds are in flight at a time (r and q alternate: a round is re-issued before the
+// other one is checked), so a granule that lands is seen about half a round trip sooner than
+// with one round waited for before the next is issued.
+__device__ __forceinline__ bool pref_check(const Pref& r, unsigned& pending, unsigned tag, float* x, int tid) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        if (((pending >> j) & 1u) && (unsigned)(r.v[j] >> 32) == tag) {
+            x[tid + j * kThreads] = __uint_as_float((unsigned)r.v[j]);
+            pending &= ~(1u << j);
+        }
+    return pending == 0;
+}
+
 __device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* x, volatile int* abort_flag,
                             const StreamFault& f, int tid, unsigned long long limit = 0,
                             const unsigned* end = nullptr, volatile int* ended = nullptr) {
@@ -101,35 +147,38 @@ __device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* 
 #pragma unroll
     for (int j = 0; j < 2; ++j)
         if (tid + j * kThreads < n) pending |= 1u << j;
-    unsigned long long start = 0;
-    for (bool first = true;; first = false) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (((pending >> j) & 1u) && (unsigned)(r.v[j] >> 32) == tag) {
-                x[tid + j * kThreads] = __uint_as_float((unsigned)r.v[j]);
-                pending &= ~(1u << j);
-            }
-        if (!pending) return true;
-        if (first) {
-            start = __builtin_amdgcn_s_memrealtime();
-        } else {
-            if (*abort_flag) return false;
-            if (end && __hip_atomic_load(end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tag) {
-                *ended = 1;
-                return false;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - start > limit) {
-                *abort_flag = 1;
-                __hip_atomic_store((gu32*)f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (f.err_host) __hip_atomic_store(f.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                return false;
-            }
-            __builtin_amdgcn_s_sleep(1);
+    if (pref_check(r, pending, tag, x, tid)) return true;  // the round issued during the last frame
+    const unsigned long long start = __builtin_amdgcn_s_memrealtime();
+    // 0: keep polling, 1: aborted / timed out, 2: the launch ended before this frame
+    auto give_up = [&]() -> int {
+        if (*abort_flag) return 1;
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        // the end word only after a while: its load would otherwise add a round trip to
+        // every poll of a frame that is merely in flight
+        if (end && now - start > kEndCheckTicks &&
+            __hip_atomic_load(end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tag) {
+            *ended = 1;
+            return 2;
         }
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if ((pending >> j) & 1u)
-                r.v[j] = __hip_atomic_load(g + tid + j * kThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (now - start > limit) {
+            *abort_flag = 1;
+            __hip_atomic_store((gu32*)f.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f.err_host) __hip_atomic_store(f.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return 1;
+        }
+        return 0;
+    };
+    Pref q;
+    pref_issue(q, g, n, tid);
+    for (;;) {
+        pref_issue(r, g, n, tid);
+        if (pref_check(q, pending, tag, x, tid)) return true;
+        if (give_up()) return false;
+        __builtin_amdgcn_s_sleep(1);
+        pref_issue(q, g, n, tid);
+        if (pref_check(r, pending, tag, x, tid)) return true;
+        if (give_up()) return false;
+        __builtin_amdgcn_s_sleep(1);
     }
 }
 
@@ -180,20 +229,6 @@ __device__ __forceinline__ void load_x(float (&xl)[KS], const float* x, int lane
         xl[i + 2] = v.z;
         xl[i + 3] = v.w;
     }
-}
-
-// value of channel slot j (< CW) in lane j: one store instruction per wave publishes them.
-// The values are wave-uniform (reduced sums), so v_writelane moves each into its lane (a
-// select chain on the lane id would be turned into a scratch-indexed array).
-template <int CW>
-__device__ __forceinline__ float lane_select(const float (&v)[CW]) {
-    int r = 0;
-#pragma unroll
-    for (int j = 0; j < CW; ++j) {
-        const int u = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v[j]));
-        asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(r) : "s"(u), "n"(j));
-    }
-    return __builtin_bit_cast(float, r);
 }
 
 __device__ __forceinline__ void trace_mark(const StreamPipeParams& p, int wg, int s, int k, int tid) {
@@ -297,40 +332,53 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         const float sc = c < c_hi ? scl[c - c_lo] : 0.f, sh = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
         for (int s = 0;; ++s) {
             const int t = t0 + s;
+            float fv = 0.f;  // element tid (< cin0) of frame t
             if (!p.serve) {
                 if (s >= p.steps) break;
+                if (tid < cin0) fv = p.frames[(int64_t)(t & (Q - 1)) * cin0 + tid];
             } else {
-                // serve: wait for frame t to be posted; end the launch on a stop request or
-                // after idle_ticks without it
-                if (tid == 0) {
-                    bool go = false;
+                // serve: thread i < cin0 polls granule i of frame t in the host ring (one PCIe
+                // round trip brings the value with its tag); thread 0 also ends the launch on a
+                // stop request or after idle_ticks without the frame
+                if (tid < cin0) {
+                    const gu64* fg = (const gu64*)p.frame_gran + (int64_t)(t & (Q - 1)) * cin0 + tid;
                     const unsigned long long start = __builtin_amdgcn_s_memrealtime();
                     for (;;) {
-                        if (__hip_atomic_load(p.posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) > (unsigned)t) {
-                            go = true;
+                        const unsigned long long x = __hip_atomic_load(fg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        if ((unsigned)(x >> 32) == (unsigned)t + 1u) {
+                            fv = __uint_as_float((unsigned)x);
                             break;
                         }
-                        if (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                            __builtin_amdgcn_s_memrealtime() - start > p.idle_ticks)
-                            break;
+                        if (__hip_atomic_load(&end_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                        if (tid == 0) {
+                            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                            if (now - start > kEndCheckTicks &&
+                                (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                                 now - start > p.idle_ticks)) {
+                                // the host writes a frame's granules before a stop request: a
+                                // granule still missing now means frame t was never posted
+                                const unsigned long long y = __hip_atomic_load(fg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                if ((unsigned)(y >> 32) == (unsigned)t + 1u) {
+                                    fv = __uint_as_float((unsigned)y);
+                                    break;
+                                }
+                                __hip_atomic_store(p.end_frame, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                __hip_atomic_store(p.ended_host, (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                                __hip_atomic_store(&end_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                break;
+                            }
+                        }
                         __builtin_amdgcn_s_sleep(1);
                     }
-                    if (!go) {
-                        __hip_atomic_store(p.end_frame, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(p.ended_host, (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                    end_flag = go ? 0 : 1;
                 }
                 __syncthreads();
                 if (end_flag) break;
             }
             trace_mark(p, wg, s, 0, tid);
             float* xv = xin + (s & 1) * kPipeExpandK;
-            const float* fr = p.frames + (int64_t)(t & (Q - 1)) * cin0;
-            for (int i = tid; i < cin0; i += kThreads) {
-                const float v = p.serve ? __uint_as_float(__hip_atomic_load((const unsigned*)fr + i, __ATOMIC_RELAXED,
-                                                                            __HIP_MEMORY_SCOPE_SYSTEM))
-                                        : fr[i];
+            if (tid < cin0) {
+                const int i = tid;
+                const float v = fv;
                 const float h1 = t == 0 ? v : hist[i];                          // frame t-1
                 const float h2 = t <= 1 ? (t == 0 ? v : h1) : hist[cin0 + i];   // frame t-2
                 xv[i] = h2;
@@ -364,15 +412,11 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         // ---- block b's k-conv: CWK rows per wave, NT = 3 taps, k-sliced ----
         uint32_t w[3][CWK][KS / 2];
         load_rows<WT, 3, CWK, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 3);
-        float sc[CWK], sh[CWK];
-        int nown = 0;
-#pragma unroll
-        for (int j = 0; j < CWK; ++j) {
-            const int c = c_lo + wid + kWaves * j;
-            sc[j] = c < c_hi ? scl[c - c_lo] : 0.f;
-            sh[j] = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
-            nown += c < c_hi;
-        }
+        // after rows_sum lane l holds row jr = l >> 4 of the wave's rows: lanes 16 jr lead
+        const int jr = lane >> 4, jq = jr < CWK ? jr : CWK - 1;
+        const int cr = c_lo + wid + kWaves * jr;
+        const bool lead = (lane & 15) == 0 && jr < CWK && cr < c_hi;
+        const float sc = lead ? scl[cr - c_lo] : 0.f, sh = lead ? scl[kPipeMaxCh + cr - c_lo] : 0.f;
         Pref pf;
         pref_issue(pf, edge(role - 1, t0), C, tid);
         for (int s = 0; p.serve || s < p.steps; ++s) {
@@ -389,60 +433,43 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             if (p.serve || s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
             float xl[KS];
             load_x<KS>(xl, xv, lane);
-            float vn[CWK], out[CWK];
-            lane_dots<WT, 3, CWK, KS>(w, xl, 2, vn);
-#pragma unroll
-            for (int j = 0; j < CWK; ++j) vn[j] = wave_sum_uniform(vn[j]);
+            float vp[CWK];
+            lane_dots<WT, 3, CWK, KS>(w, xl, 2, vp);
+            const float vn = rows_sum<CWK>(vp, lane);  // newest tap, row jr
             const int slot = t & (R - 1);
             if (t == 0) {
                 // every tap reads x(0); outputs 1..2d start from the taps that still reach
                 // before the stream start
-                float v0[CWK], v1[CWK];
-                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0);
-                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1);
-#pragma unroll
-                for (int j = 0; j < CWK; ++j) {
-                    v0[j] = wave_sum_uniform(v0[j]);
-                    v1[j] = wave_sum_uniform(v1[j]);
-                    out[j] = (v0[j] + v1[j]) + vn[j];
-                    float y = out[j] * sc[j] + sh[j];
-                    out[j] = y > 0.f ? y : 0.f;
-                }
-                if (lane < nown)
-                    publish(out_edge(role, t) + c_lo + wid + kWaves * lane, (unsigned)t + 1u, lane_select<CWK>(out));
+                float v0p[CWK], v1p[CWK];
+                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0p);
+                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1p);
+                const float v0 = rows_sum<CWK>(v0p, lane), v1 = rows_sum<CWK>(v1p, lane);
+                const float y = ((v0 + v1) + vn) * sc + sh;
+                if (lead) publish(out_edge(role, t) + cr, (unsigned)t + 1u, y > 0.f ? y : 0.f);
                 trace_mark(p, wg, s, 1, tid);
                 // ring: all slots zero, then outputs tt = 1..2d from the clamped taps
                 for (int i = lane; i < R * CWK; i += 64) wring[i] = 0.f;
-                if (lane < CWK) {
+                if (lead) {
                     for (int tt = 1; tt <= 2 * d; ++tt) {
                         float a = 0.f;
-                        if (2 * d >= tt) a += lane_select<CWK>(v0);
-                        if (d >= tt) a += lane_select<CWK>(v1);
-                        wring[(tt & (R - 1)) * CWK + lane] = a;
+                        if (2 * d >= tt) a += v0;
+                        if (d >= tt) a += v1;
+                        wring[(tt & (R - 1)) * CWK + jq] = a;
                     }
                 }
             } else {
-#pragma unroll
-                for (int j = 0; j < CWK; ++j) {
-                    float y = (wring[slot * CWK + j] + vn[j]) * sc[j] + sh[j];
-                    out[j] = y > 0.f ? y : 0.f;
-                }
-                if (lane < nown)
-                    publish(out_edge(role, t) + c_lo + wid + kWaves * lane, (unsigned)t + 1u, lane_select<CWK>(out));
+                const float y = (wring[slot * CWK + jq] + vn) * sc + sh;
+                if (lead) publish(out_edge(role, t) + cr, (unsigned)t + 1u, y > 0.f ? y : 0.f);
                 trace_mark(p, wg, s, 1, tid);
                 // the older taps of x(t) feed outputs t + d (tap 1) and t + 2d (tap 0)
-                float v0[CWK], v1[CWK];
-                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1);
-                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0);
-#pragma unroll
-                for (int j = 0; j < CWK; ++j) {
-                    v1[j] = wave_sum_uniform(v1[j]);
-                    v0[j] = wave_sum_uniform(v0[j]);
-                }
-                if (lane < CWK) {
-                    wring[slot * CWK + lane] = 0.f;
-                    wring[((t + d) & (R - 1)) * CWK + lane] += lane_select<CWK>(v1);
-                    wring[((t + 2 * d) & (R - 1)) * CWK + lane] += lane_select<CWK>(v0);
+                float v0p[CWK], v1p[CWK];
+                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1p);
+                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0p);
+                const float v1 = rows_sum<CWK>(v1p, lane), v0 = rows_sum<CWK>(v0p, lane);
+                if (lead) {
+                    wring[slot * CWK + jq] = 0.f;
+                    wring[((t + d) & (R - 1)) * CWK + jq] += v1;
+                    wring[((t + 2 * d) & (R - 1)) * CWK + jq] += v0;
                 }
             }
         }
@@ -452,15 +479,10 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         // ---- block b's 1x1 conv (+ residual x_b(t)) or the shrink: CWP rows per wave ----
         uint32_t w[1][CWP][KS / 2];
         load_rows<WT, 1, CWP, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 1);
-        float sc[CWP], sh[CWP];
-        int nown = 0;
-#pragma unroll
-        for (int j = 0; j < CWP; ++j) {
-            const int c = c_lo + wid + kWaves * j;
-            sc[j] = c < c_hi ? scl[c - c_lo] : 0.f;
-            sh[j] = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
-            nown += c < c_hi;
-        }
+        // after rows_sum lane l holds row l >> 3 of the wave's rows: lanes 8 j lead
+        const int cr = c_lo + wid + kWaves * (lane >> 3);
+        const bool lead = (lane & 7) == 0 && cr < c_hi;
+        const float sc = lead ? scl[cr - c_lo] : 0.f, sh = lead ? scl[kPipeMaxCh + cr - c_lo] : 0.f;
         const int nres = is_p ? c_hi - c_lo : 0;
         Pref pf, pr;
         pref_issue(pr, edge(role - 2, t0) + c_lo, nres, tid);
@@ -485,36 +507,22 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             }
             float xl[KS];
             load_x<KS>(xl, xv, lane);
-            float v[CWP], out[CWP];
-            lane_dots<WT, 1, CWP, KS>(w, xl, 0, v);
-#pragma unroll
-            for (int j = 0; j < CWP; ++j) {
-                v[j] = wave_sum_uniform(v[j]);
-                const int c = c_lo + wid + kWaves * j;
-                float y = v[j] * sc[j] + sh[j];
+            float vp[CWP];
+            lane_dots<WT, 1, CWP, KS>(w, xl, 0, vp);
+            float y = rows_sum<CWP>(vp, lane) * sc + sh;
+            if (lead) {
                 if (is_p) {
                     y = y > 0.f ? y : 0.f;
-                    y += c < c_hi ? rv[c - c_lo] : 0.f;
+                    y += rv[cr - c_lo];
+                    publish(out_edge(role, t) + cr, (unsigned)t + 1u, y);
+                } else if (p.serve) {
+                    // host-mapped pose ring: the granule's tag tells the host it is there
+                    const unsigned long long g = ((unsigned long long)((unsigned)t + 1u) << 32) | __float_as_uint(y);
+                    __hip_atomic_store(p.pose_gran + (int64_t)(t & (Q - 1)) * Nout + cr, g, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                } else {
+                    p.poses[(int64_t)(t & (Q - 1)) * Nout + cr] = y;
                 }
-                out[j] = y;
-            }
-            if (lane < nown) {
-                const float y = lane_select<CWP>(out);
-                const int c = c_lo + wid + kWaves * lane;
-                if (is_p)
-                    publish(out_edge(role, t) + c, (unsigned)t + 1u, y);
-                else if (p.serve)  // host-mapped pose ring
-                    __hip_atomic_store((unsigned*)p.poses + (int64_t)(t & (Q - 1)) * Nout + c, __float_as_uint(y),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                else
-                    p.poses[(int64_t)(t & (Q - 1)) * Nout + c] = y;
-            }
-            if (p.serve && !is_p) {
-                // this workgroup's pose channels of frame t are in host memory: report it
-                __threadfence_system();
-                __syncthreads();
-                if (tid == 0)
-                    __hip_atomic_store(p.done_host + gi, (unsigned)t + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             trace_mark(p, wg, s, 1, tid);
         }

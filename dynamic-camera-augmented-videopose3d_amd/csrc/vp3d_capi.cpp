@@ -791,11 +791,11 @@ struct vp3d_stream {
     unsigned long long spin_ticks = kStreamSpinTicks;
     // serve form (pipe only): pinned host rings + control words, and the device end word
     bool serving = false;
-    void* serve_host = nullptr;        // [ctrl: posted, stop, pad.., done[16]][frames Q x cin][poses Q x nout]
+    void* serve_host = nullptr;        // [ctrl: -, stop, ended][frame granules Q x cin][pose granules Q x nout]
     void* serve_dev = nullptr;         // device view of serve_host
     unsigned* end_frame = nullptr;     // device word
     int64_t posted = 0;                // host: frames posted so far (absolute)
-    int n_done = 0;                    // shrink workgroups reporting
+    int64_t done_seen = 0;             // host: frames whose pose granules were all seen
     hipStream_t serve_stream = nullptr;
 };
 
@@ -1232,21 +1232,27 @@ int vp3d_stream_graph_launch(vp3d_stream* st, void* stream) {
 }  // extern "C"
 
 namespace {
-constexpr int kServeCtrlWords = 32;  // [0] posted, [1] stop, [2] ended (+1), [16 ..] done per shrink workgroup
+constexpr int kServeCtrlWords = 32;  // [1] stop, [2] ended (+1); 128 bytes, so the rings stay 8-byte aligned
 unsigned* serve_ctrl(vp3d_stream* st) { return (unsigned*)st->serve_host; }
-float* serve_frames(vp3d_stream* st) { return (float*)((char*)st->serve_host + kServeCtrlWords * 4); }
-float* serve_poses(vp3d_stream* st) {
-    return serve_frames(st) + (size_t)kQueue * st->h->layers[0].cin;
-}
+// {tag = frame + 1, f32 bits} granules: frame t in slot t % Q of each ring
+uint64_t* serve_frames(vp3d_stream* st) { return (uint64_t*)((char*)st->serve_host + kServeCtrlWords * 4); }
+uint64_t* serve_poses(vp3d_stream* st) { return serve_frames(st) + (size_t)kQueue * st->h->layers[0].cin; }
 template <typename T>
 T* dev_view(vp3d_stream* st, T* host_ptr) {
     return (T*)((char*)st->serve_dev + ((char*)host_ptr - (char*)st->serve_host));
 }
-unsigned serve_done_min(vp3d_stream* st) {
-    const volatile unsigned* done = serve_ctrl(st) + 16;
-    unsigned m = done[0];
-    for (int i = 1; i < st->n_done; ++i) m = std::min(m, (unsigned)done[i]);
-    return m;
+// every pose granule of frame f carries its tag (the shrink workgroups store them last)
+bool serve_pose_ready(vp3d_stream* st, int64_t f) {
+    const int nout = st->h->layers.back().cout;
+    const uint64_t* g = serve_poses(st) + (size_t)(f % kQueue) * nout;
+    for (int i = 0; i < nout; ++i)
+        if ((uint32_t)(__atomic_load_n(g + i, __ATOMIC_RELAXED) >> 32) != (uint32_t)(f + 1)) return false;
+    return true;
+}
+// frames complete in order: advance the host's count of finished frames
+int64_t serve_done(vp3d_stream* st) {
+    while (st->done_seen < st->posted && serve_pose_ready(st, st->done_seen)) ++st->done_seen;
+    return st->done_seen;
 }
 }  // namespace
 
@@ -1260,11 +1266,8 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     if (!(idle_ms > 0.0) || idle_ms > 1000.0) return fail(VP3D_ERR_ARG, "idle_ms must be in (0, 1000]");
     hipStream_t s = (hipStream_t)stream;
     const vp3d_handle* h = st->h;
-    const int nl = (int)h->layers.size();
-    st->n_done = st->pipe_p.cu0[nl] - st->pipe_p.cu0[nl - 1];
-    if (st->n_done > 16) return fail(VP3D_ERR_STATE, "too many shrink workgroups to report");
+    const size_t bytes = kServeCtrlWords * 4 + (size_t)kQueue * (h->layers[0].cin + h->layers.back().cout) * 8;
     if (!st->serve_host) {
-        const size_t bytes = kServeCtrlWords * 4 + (size_t)kQueue * (h->layers[0].cin + h->layers.back().cout) * 4;
         HIP_TRY(hipHostMalloc(&st->serve_host, bytes, hipHostMallocMapped));
         HIP_TRY(hipHostGetDevicePointer(&st->serve_dev, st->serve_host, 0));
         HIP_TRY(hipMalloc(&st->end_frame, 4));
@@ -1275,19 +1278,15 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     HIP_TRY(hipMemcpy(&pos, st->frames_seen, 4, hipMemcpyDeviceToHost));
     st->host_t = pos;
     st->posted = pos;
-    volatile unsigned* ctrl = serve_ctrl(st);
-    ctrl[0] = (unsigned)pos;
-    ctrl[1] = 0u;
-    ctrl[2] = 0u;
-    for (int i = 0; i < 16; ++i) ctrl[16 + i] = (unsigned)pos;
+    st->done_seen = pos;
+    // no granule of an earlier session (or of frames before a reset) may carry a tag of this one
+    std::memset(st->serve_host, 0, bytes);
     HIP_TRY(hipMemsetAsync(st->end_frame, 0xff, 4, s));
     StreamPipeParams p = st->pipe_p;
     p.serve = 1;
-    p.frames = dev_view(st, serve_frames(st));
-    p.poses = dev_view(st, serve_poses(st));
-    p.posted = dev_view(st, serve_ctrl(st));
+    p.frame_gran = (const unsigned long long*)dev_view(st, serve_frames(st));
+    p.pose_gran = (unsigned long long*)dev_view(st, serve_poses(st));
     p.stop = dev_view(st, serve_ctrl(st) + 1);
-    p.done_host = dev_view(st, serve_ctrl(st) + 16);
     p.ended_host = dev_view(st, serve_ctrl(st) + 2);
     p.end_frame = st->end_frame;
     p.idle_ticks = (unsigned long long)(idle_ms * 1e5);  // 100 MHz clock
@@ -1304,14 +1303,18 @@ int vp3d_stream_serve_post(vp3d_stream* st, const float* frame, int64_t* frame_i
     if (!st->serving) return fail(VP3D_ERR_STATE, "not serving (vp3d_stream_serve_begin)");
     if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
     if (((volatile unsigned*)serve_ctrl(st))[2]) return fail(VP3D_ERR_STATE, "the serve launch ended (idle); vp3d_stream_serve_end, then begin");
-    if (st->posted - (int64_t)serve_done_min(st) >= kQueue - 1)
+    if (st->posted - serve_done(st) >= kQueue - 1)
         return fail(VP3D_ERR_STATE, "serve ring full: wait for earlier frames first");
     const int cin = st->h->layers[0].cin;
     const int64_t t = st->posted;
-    std::memcpy(serve_frames(st) + (size_t)(t % kQueue) * cin, frame, 4 * (size_t)cin);
-    // the frame's bytes before the count (x86 stores are ordered; the release keeps the
-    // compiler from reordering them)
-    __atomic_store_n(serve_ctrl(st), (unsigned)(t + 1), __ATOMIC_RELEASE);
+    // one 8-byte store per value: the expand workgroups poll these granules themselves
+    uint64_t* g = serve_frames(st) + (size_t)(t % kQueue) * cin;
+    const uint64_t tag = (uint64_t)(uint32_t)(t + 1) << 32;
+    for (int i = 0; i < cin; ++i) {
+        uint32_t bits;
+        std::memcpy(&bits, frame + i, 4);
+        __atomic_store_n(g + i, tag | bits, __ATOMIC_RELAXED);
+    }
     st->posted = t + 1;
     if (frame_index) *frame_index = t;
     return VP3D_OK;
@@ -1322,22 +1325,22 @@ int vp3d_stream_serve_wait(vp3d_stream* st, int64_t frame_index, float* pose, do
     if (!st->serving) return fail(VP3D_ERR_STATE, "not serving (vp3d_stream_serve_begin)");
     if (frame_index < 0 || frame_index >= st->posted) return fail(VP3D_ERR_ARG, "frame was not posted");
     if (st->posted - frame_index >= kQueue) return fail(VP3D_ERR_ARG, "frame's pose slot was reused");
-    const volatile unsigned* done = serve_ctrl(st) + 16;
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
-        bool all = true;
-        for (int i = 0; i < st->n_done; ++i)
-            if ((int64_t)done[i] <= frame_index) all = false;
-        if (all) break;
+        if (serve_pose_ready(st, frame_index)) break;
         if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
         const unsigned ended = ((volatile unsigned*)serve_ctrl(st))[2];
         if (ended && (int64_t)ended - 1 <= frame_index) return fail(VP3D_ERR_STATE, "the serve launch ended before this frame");
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (ms > timeout_ms) return fail(VP3D_ERR_STATE, "serve wait timed out (the launch ended or is stalled)");
     }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
     const int nout = st->h->layers.back().cout;
-    if (pose) std::memcpy(pose, serve_poses(st) + (size_t)(frame_index % kQueue) * nout, 4 * (size_t)nout);
+    const uint64_t* g = serve_poses(st) + (size_t)(frame_index % kQueue) * nout;
+    if (pose)
+        for (int i = 0; i < nout; ++i) {
+            const uint32_t bits = (uint32_t)__atomic_load_n(g + i, __ATOMIC_RELAXED);
+            std::memcpy(pose + i, &bits, 4);
+        }
     return VP3D_OK;
 }
 

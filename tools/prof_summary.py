@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"conv_gemm_(h16|f32)[^(]*", name)
+    m = re.search(r"(conv_gemm_(h16|f32|q64|q4w|8p)|expand_gemm_h16)[^(]*", name)
     if m:
         return m.group(0)[:80]
     return name[:80]
@@ -74,7 +74,9 @@ def per_layer(trace, B):
             rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], int(r["Grid_Size_X"]),
                          (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     rows.sort()
-    eg = ((B * 81 + 255) // 256) * 256
+    # the expand grid of the largest forward in the trace (the bench's batch; the 16-bit
+    # expand's grid depends on its row-block form, so it is not derived from B)
+    eg = max((r[2] for r in rows if "expand_gemm" in r[1]), default=0)
     agg = defaultdict(list)
     names = {}
     i = 0

@@ -60,21 +60,23 @@ def main():
             c = clk[first[i]:first[i + 1], s]
             if not c.all():
                 break
-            r[n] = ((int(c[:, 0].max()) - base) / 100.0, (int(c[:, 1].max()) - base) / 100.0)
+            r[n] = ((int(c[:, 0].max()) - base) / 100.0, (int(c[:, 1].max()) - base) / 100.0,
+                    (int(c[:, 0].min()) - base) / 100.0, (int(c[:, 1].min()) - base) / 100.0)
         rows.append(r)
     skip = min(8, len(rows) // 2)  # first frames: weights to VGPRs, clocks up
     steady = rows[skip:]
     med = {"wall_us": float(np.median([r["wall_us"] for r in steady]))}
     for n in names:
         if all(n in r for r in steady):
-            med[n] = (float(np.median([r[n][0] for r in steady])), float(np.median([r[n][1] for r in steady])))
-    print("role: input complete / first output stored, us after the expand role saw the frame (median of "
-          f"{len(steady)} frames)")
+            med[n] = tuple(float(np.median([r[n][k] for r in steady])) for k in range(4))
+    print("role: input complete / first output stored by the LAST (first) workgroup of the role, us after the "
+          f"first expand workgroup had the frame (median of {len(steady)} frames)")
     prev = 0.0
     for n in names:
         if n in med:
-            i, o = med[n]
-            print(f"  {n:7s} in {i:7.2f}  out {o:7.2f}   (hand-off {i - prev:5.2f}, compute {o - i:5.2f})")
+            i, o, i0, o0 = med[n]
+            print(f"  {n:7s} in {i:7.2f} ({i0:6.2f})  out {o:7.2f} ({o0:6.2f})   "
+                  f"(hand-off {i - prev:5.2f}, compute {o - i:5.2f})")
             prev = o
     print(f"  host wall (post -> pose in host memory): {med['wall_us']:.2f} us")
     if a.out:

@@ -1,3 +1,7 @@
+// RETIRED (not built): measured on MI355X (gpurun_out r03g, B = 65,536 bf16): bit-identical
+// output, block-1 k3 40.2 ms vs 9.2 ms on conv_gemm_q64, every q64 layer 3.3-3.9x slower.  At
+// one wave per SIMD the 256 AGPR accumulators plus two fragment sets leave the compiler 201
+// VGPR spills (the LDS address registers reloaded from scratch inside the K loop).
 // 256x256 conv-GEMM at ONE wave per SIMD: 4 waves, each owning a 128 x 128 output tile
 // (16-bit operands, 16-bit output).
 //
