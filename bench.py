@@ -177,16 +177,17 @@ def stream_main(args, world, rank, dev):
         e1.synchronize()
         lat.append(e0.elapsed_time(e1) * 1e3)
     # real-time serving, ONE frame in flight: host frame in -> host pose out, wall clock
-    serve_lat = None
+    serve_lat = serve_py = None
     if mode == "pipe":
         frames_h = xs[0].cpu().numpy()
-        serve_lat = []
+        serve_lat, serve_py = [], []
         with st.serve(idle_ms=200.0) as sv:
             for i in range(32 + 512):
                 t0 = time.perf_counter_ns()
                 sv.step(frames_h[i % T])
                 if i >= 32:  # after the first frames (weights to VGPRs, clocks up)
-                    serve_lat.append((time.perf_counter_ns() - t0) * 1e-3)
+                    serve_py.append((time.perf_counter_ns() - t0) * 1e-3)
+                    serve_lat.append(sv.last_latency_us)
     pad = (RF_FULL - 1) // 2
     xp = torch.cat([xs[:, :1].expand(1, 2 * pad, -1, -1), xs], dim=1).cpu()
     ref = lifter_forward(sd, xp, FW, causal=True).numpy()[0]
@@ -238,14 +239,16 @@ def stream_main(args, world, rank, dev):
         "cpu_baseline": cpu,
         "single_step_latency_us": round(float(np.median(serve_lat if serve_lat else lat)), 2),
         "single_step_latency_note": ("serve form: one frame in flight, host frame posted to pinned memory -> pose "
-                                     "back in host memory, wall clock, median of 512 (resident launch, "
-                                     "vp3d_stream_serve_*)" if serve_lat else
+                                     "back in host memory, the library's wall clock around post + wait "
+                                     "(vp3d_stream_serve_step; resident launch), median of 512; "
+                                     "serve_python_latency_us adds the Python/ctypes call" if serve_lat else
                                      "eager launch of one step from an idle stream (HIP events)"),
         "serve_latency_us": ({"median": round(float(np.median(serve_lat)), 2),
                               "p90": round(float(np.percentile(serve_lat, 90)), 2),
                               "p99": round(float(np.percentile(serve_lat, 99)), 2),
                               "frames_per_s_one_in_flight": round(1e6 / float(np.median(serve_lat)), 1)}
                              if serve_lat else None),
+        "serve_python_latency_us": round(float(np.median(serve_py)), 2) if serve_py else None,
         "eager_step_latency_us": round(float(np.median(lat)), 2),
         "parity": {"frames": T, f"{args.dtype}_max_coord_delta_mm": float(np.abs(outs - ref).max()) * 1e3,
                    f"{args.dtype}_mpjpe_delta_mm": abs(mp(outs) - mp(ref)) * 1e3},

@@ -165,6 +165,7 @@ constexpr int kPipeCwK = 3;        // k-conv rows per wave (3 taps each)
 constexpr int kPipeCwP = 8;        // 1x1 / shrink rows per wave
 constexpr int kPipeMaxCh = 512;    // channels per workgroup (expand: one per lane of 8 waves)
 constexpr int kPipeExpandK = 128;  // expand K (3 frames x J_in*F, zero-padded)
+constexpr int kStreamTraceSlots = 11;  // input complete, one per wave of the 512-thread workgroup, 2 shader clocks
 struct StreamPipeParams {
     const void* W[kStreamMaxLayers];       // packed 16-bit weights [Np][Kp], tap-major K
     const float* scale[kStreamMaxLayers];  // folded BatchNorm (shrink: 1 / bias)
@@ -178,7 +179,10 @@ struct StreamPipeParams {
     float* poses;                          // pose ring (queue slots of N[nl-1] floats)
     int* frames_seen;                      // stream position (read at start, advanced by the last workgroup)
     unsigned* arrivals;                    // end-of-launch arrival counter (zero between launches)
-    unsigned long long* gran;              // [queue][2nb+1 edges][C] granules
+    unsigned long long* gran;              // [queue][2nb+1 edges][C / 64 chunks x chunk_stride] granules
+    int chunk_stride;                      // granules between the 64-granule chunks of an edge (>= 64)
+    int poll_rounds, poll_pause;           // poll rounds in flight (1, 2); s_sleep 1 pauses between rounds
+    int row_contig;                        // a wave's rows contiguous (1) or kWaves apart (0)
     StreamFault fault;                     // sticky timeout word
     float* state;                          // [workgroups][state_stride]: k-conv rings / expand history
     int state_stride;
@@ -198,9 +202,10 @@ struct StreamPipeParams {
     unsigned* end_frame;
     unsigned* ended_host;                  // host-mapped copy of the end frame + 1 (0 while serving)
     unsigned long long idle_ticks;
-    // diagnostics (VP3D_STREAM_TRACE=n at vp3d_stream_create): thread 0 of every workgroup
-    // records the 100 MHz clock when the input of its frame s < trace_frames is complete and
-    // after its first output store: trace[(wg * trace_frames + s) * 2 + {0, 1}]
+    // diagnostics (VP3D_STREAM_TRACE=n at vp3d_stream_create): every workgroup records the
+    // 100 MHz clock when the input of its frame s < trace_frames is complete (slot 0) and, per
+    // wave w, after the wave's first output store (slot 1 + w):
+    // trace[(wg * trace_frames + s) * kStreamTraceSlots + slot]
     unsigned long long* trace;
     int trace_frames;
 };

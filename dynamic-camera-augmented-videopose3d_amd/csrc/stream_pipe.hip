@@ -57,6 +57,16 @@ __device__ __forceinline__ float hi16(uint32_t w) {
     return (float)__builtin_bit_cast(WT, (unsigned short)(w >> 16));
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// 16-bit weight pair -> two f32 (exact), converted once when the weights are loaded: the
+// dot products then run as v_pk_fma_f32 (two FMAs per instruction) on f32 pairs instead of a
+// convert + FMA per element every frame
+template <typename WT>
+__device__ __forceinline__ f2 widen2(uint32_t w) {
+    return f2{lo16<WT>(w), hi16<WT>(w)};
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
@@ -107,28 +117,32 @@ __device__ __forceinline__ void publish(gu64* g, unsigned tag, float v) {
     __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Granule slice of an edge: element c lives at base + (c0 + c) / 64 * cs + (c0 + c) % 64, i.e.
+// 64-granule (512-byte) chunks cs granules apart (cs = 64: contiguous; larger: every chunk
+// on its own 4 KB page, so the polls of one edge spread over more memory channels)
+struct EdgeRef {
+    const gu64* base;
+    int c0, cs;
+    __device__ __forceinline__ const gu64* at(int c) const { return base + ((c0 + c) >> 6) * cs + ((c0 + c) & 63); }
+};
+
 // A sweep split in two so that the next frame's granule loads are in flight while the
 // current frame computes: pref_issue loads this thread's granules (tid, tid + kThreads of
 // an edge slice of n <= 2 * kThreads), pref_finish checks their tags, re-polls the ones
 // still missing (bounded, as sweep) and stores the values into x (LDS).
-constexpr unsigned long long kEndCheckTicks = 1000;  // 10 us of the 100 MHz clock
-
 struct Pref {
     unsigned long long v[2];
 };
 
-__device__ __forceinline__ void pref_issue(Pref& r, const gu64* g, int n, int tid) {
+constexpr unsigned long long kEndCheckTicks = 1000;  // 10 us of the 100 MHz clock
+
+__device__ __forceinline__ void pref_issue(Pref& r, const EdgeRef& e, int n, int tid, unsigned mask = 3u) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-        if (tid + j * kThreads < n) r.v[j] = __hip_atomic_load(g + tid + j * kThreads, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (((mask >> j) & 1u) && tid + j * kThreads < n)
+            r.v[j] = __hip_atomic_load(e.at(tid + j * kThreads), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// true once every granule carried `tag`; false on timeout (sets the fault words) or when
-// another wave aborted, or -- serve form -- once the launch ended before frame tag - 1
-// (*end < tag: that frame is never produced; *ended is then set).
-// Two poll rounds are in flight at a time (r and q alternate: a round is re-issued before the
-// other one is checked), so a granule that lands is seen about half a round trip sooner than
-// with one round waited for before the next is issued.
 __device__ __forceinline__ bool pref_check(const Pref& r, unsigned& pending, unsigned tag, float* x, int tid) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -139,8 +153,18 @@ __device__ __forceinline__ bool pref_check(const Pref& r, unsigned& pending, uns
     return pending == 0;
 }
 
-__device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* x, volatile int* abort_flag,
-                            const StreamFault& f, int tid, unsigned long long limit = 0,
+__device__ __forceinline__ void poll_pause(int n) {
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
+}
+
+// true once every granule carried `tag`; false on timeout (sets the fault words) or when
+// another wave aborted, or -- serve form -- once the launch ended before frame tag - 1
+// (*end < tag: that frame is never produced; *ended is then set).
+// rounds = 1: one poll of the missing granules in flight, waited for before the next;
+// rounds = 2: two rounds in flight (r and q alternate, each re-issued before the other is
+// checked).  `pause` x s_sleep 1 between rounds.
+__device__ bool pref_finish(Pref& r, const EdgeRef& e, int n, unsigned tag, float* x, volatile int* abort_flag,
+                            const StreamFault& f, int tid, int rounds, int pause, unsigned long long limit = 0,
                             const unsigned* end = nullptr, volatile int* ended = nullptr) {
     if (limit == 0) limit = f.spin_ticks;
     unsigned pending = 0;
@@ -168,72 +192,89 @@ __device__ bool pref_finish(Pref& r, const gu64* g, int n, unsigned tag, float* 
         }
         return 0;
     };
+    if (rounds < 2) {
+        for (;;) {
+            pref_issue(r, e, n, tid, pending);
+            if (pref_check(r, pending, tag, x, tid)) return true;
+            if (give_up()) return false;
+            poll_pause(pause);
+        }
+    }
     Pref q;
-    pref_issue(q, g, n, tid);
+    pref_issue(q, e, n, tid, pending);
     for (;;) {
-        pref_issue(r, g, n, tid);
+        pref_issue(r, e, n, tid, pending);
         if (pref_check(q, pending, tag, x, tid)) return true;
         if (give_up()) return false;
-        __builtin_amdgcn_s_sleep(1);
-        pref_issue(q, g, n, tid);
+        poll_pause(pause);
+        pref_issue(q, e, n, tid, pending);
         if (pref_check(r, pending, tag, x, tid)) return true;
         if (give_up()) return false;
-        __builtin_amdgcn_s_sleep(1);
+        poll_pause(pause);
     }
 }
 
-// Lane-partial dot products of the wave's CW rows (NT taps each) with the lane's KS
-// input elements xl: s[tap][j] = sum_i w[tap][j][i] * xl[i].
-template <typename WT, int NT, int CW, int KS>
-__device__ __forceinline__ void lane_dots(const uint32_t (&w)[NT][CW][KS / 2], const float (&xl)[KS], int tap,
+// Lane-partial dot products of the wave's CW rows (NT taps each) with the lane's KS input
+// elements xl (as KS/2 pairs): s[j] = sum_i w[tap][j][i] . xl[i], even and odd elements in
+// the two halves of one v_pk_fma_f32 chain, added at the end.
+template <int NT, int CW, int KS>
+__device__ __forceinline__ void lane_dots(const f2 (&w)[NT][CW][KS / 2], const f2 (&xl)[KS / 2], int tap,
                                           float (&s)[CW]) {
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
-        float a = 0.f;
+        f2 a = f2{0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < KS / 2; ++i) {
-            a = __builtin_fmaf(lo16<WT>(w[tap][j][i]), xl[2 * i], a);
-            a = __builtin_fmaf(hi16<WT>(w[tap][j][i]), xl[2 * i + 1], a);
-        }
-        s[j] = a;
+        for (int i = 0; i < KS / 2; ++i) a = __builtin_elementwise_fma(w[tap][j][i], xl[i], a);
+        s[j] = a.x + a.y;
     }
 }
 
-// Load the wave's rows of one layer into registers: row c = c_lo + wid + kWaves * j, tap
+// Row j (< CW) of wave w: contiguous (c_lo + CW w + j: a wave's results are neighbouring
+// granules, 8 rows = one 64-byte line written by one store) or strided (c_lo + w + 8 j).
+template <int CW>
+__device__ __forceinline__ int row_of(int c_lo, int wid, int j, int contig) {
+    return contig ? c_lo + CW * wid + j : c_lo + wid + kWaves * j;
+}
+
+// Load the wave's rows of one layer into registers: row c = row_of(j), tap
 // segment [tap * C + lane * KS, +KS) of the [Np][Kp] 16-bit matrix (rows past c_hi: zero).
 template <typename WT, int NT, int CW, int KS>
-__device__ __forceinline__ void load_rows(uint32_t (&w)[NT][CW][KS / 2], const WT* W, int Kp, int C, int c_lo,
-                                          int c_hi, int wid, int lane, int taps) {
+__device__ __forceinline__ void load_rows(f2 (&w)[NT][CW][KS / 2], const WT* W, int Kp, int C, int c_lo, int c_hi,
+                                          int wid, int lane, int taps, int contig) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int j = 0; j < CW; ++j) {
-            const int c = c_lo + wid + kWaves * j;
+            const int c = row_of<CW>(c_lo, wid, j, contig);
 #pragma unroll
-            for (int i = 0; i < KS / 2; ++i) w[t][j][i] = 0u;
+            for (int i = 0; i < KS / 2; ++i) w[t][j][i] = f2{0.f, 0.f};
             if (c < c_hi && t < taps) {
                 const uint32_t* src = (const uint32_t*)(W + (int64_t)c * Kp + t * C + lane * KS);
 #pragma unroll
-                for (int i = 0; i < KS / 2; ++i) w[t][j][i] = src[i];
+                for (int i = 0; i < KS / 2; ++i) w[t][j][i] = widen2<WT>(src[i]);
             }
         }
 }
 
 template <int KS>
-__device__ __forceinline__ void load_x(float (&xl)[KS], const float* x, int lane) {
+__device__ __forceinline__ void load_x(f2 (&xl)[KS / 2], const float* x, int lane) {
 #pragma unroll
     for (int i = 0; i < KS; i += 4) {
         const float4 v = *(const float4*)(x + lane * KS + i);
-        xl[i] = v.x;
-        xl[i + 1] = v.y;
-        xl[i + 2] = v.z;
-        xl[i + 3] = v.w;
+        xl[i / 2] = f2{v.x, v.y};
+        xl[i / 2 + 1] = f2{v.z, v.w};
     }
 }
 
 __device__ __forceinline__ void trace_mark(const StreamPipeParams& p, int wg, int s, int k, int tid) {
-    if (p.trace && tid == 0 && s < p.trace_frames)
-        p.trace[((int64_t)wg * p.trace_frames + s) * 2 + k] = __builtin_amdgcn_s_memrealtime();
+    // k = 0: thread 0 once the frame's input is complete (slot 0, and the shader clock in
+    // slot 9); k = 1: lane 0 of each wave after its first output store (slot 1 + wave; wave 0
+    // also the shader clock in slot 10)
+    if (p.trace && s < p.trace_frames && (k ? (tid & 63) == 0 : tid == 0)) {
+        unsigned long long* e = p.trace + ((int64_t)wg * p.trace_frames + s) * kStreamTraceSlots;
+        e[k ? 1 + (tid >> 6) : 0] = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0) e[k ? 10 : 9] = __builtin_amdgcn_s_memtime();
+    }
 }
 
 }  // namespace
@@ -276,7 +317,10 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     // arrival, no position advance), so nothing drifts out of step
     if (__hip_atomic_load(p.fault.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     K0 = p.Kp[0];
-    const int c_lo = (int)((int64_t)N * gi / gn), c_hi = (int)((int64_t)N * (gi + 1) / gn);
+    // a role's channels split over its workgroups in units of 8 (one 64-byte line of granules)
+    const int nu = (N + 7) >> 3;
+    const int c_lo = 8 * (int)((int64_t)nu * gi / gn), c_hi = min(N, 8 * (int)((int64_t)nu * (gi + 1) / gn));
+    const int contig = p.row_contig;
     const bool is_expand = role == 0, is_shrink = role == nl - 1;
     const bool is_k = !is_expand && !is_shrink && (role & 1);
     const bool is_p = !is_expand && !is_shrink && !(role & 1);
@@ -314,22 +358,35 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     const int t0 = *p.frames_seen;
     __syncthreads();
 
-    auto edge = [&](int e, int t) { return (const gu64*)p.gran + ((int64_t)(t & (Q - 1)) * nE + e) * C; };
-    auto out_edge = [&](int e, int t) { return (gu64*)p.gran + ((int64_t)(t & (Q - 1)) * nE + e) * C; };
+    const int cs = p.chunk_stride;  // granules between 64-granule chunks of an edge
+    const int64_t edge_len = (int64_t)(C >> 6) * cs;
+    auto edge = [&](int e, int t, int c0 = 0) {
+        return EdgeRef{(const gu64*)p.gran + ((int64_t)(t & (Q - 1)) * nE + e) * edge_len, c0, cs};
+    };
+    auto out_at = [&](int e, int t, int c) {
+        return (gu64*)p.gran + ((int64_t)(t & (Q - 1)) * nE + e) * edge_len + (c >> 6) * cs + (c & 63);
+    };
+    const int rounds = p.poll_rounds, pause = p.poll_pause;
 
     if (is_expand) {
         // ---- lane per channel: row c = c_lo + 64 wid + lane, Kp0 (<= 128) 16-bit weights ----
         const int cin0 = p.cin0;
         const int c = c_lo + wid * 64 + lane;
-        uint32_t w[kPipeExpandK / 2];
+        f2 w[kPipeExpandK / 2];
 #pragma unroll
-        for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = 0u;
+        for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = f2{0.f, 0.f};
         if (c < c_hi) {
             const uint32_t* src = (const uint32_t*)((const WT*)Wr + (int64_t)c * K0);
 #pragma unroll
-            for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = 2 * i < K0 ? src[i] : 0u;  // K0 <= kPipeExpandK
+            for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = widen2<WT>(2 * i < K0 ? src[i] : 0u);  // K0 <= kPipeExpandK
         }
         const float sc = c < c_hi ? scl[c - c_lo] : 0.f, sh = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
+        // thread i < cin0 owns input element i: frames t-1, t-2 of it stay in registers (hist
+        // in LDS only carries them across launches); the padding of both input buffers is
+        // written once
+        float hp1 = tid < cin0 ? hist[tid] : 0.f, hp2 = tid < cin0 ? hist[cin0 + tid] : 0.f;
+        for (int i = 3 * cin0 + tid; i < 2 * kPipeExpandK; i += kThreads)
+            if (i % kPipeExpandK >= 3 * cin0) xin[i] = 0.f;
         for (int s = 0;; ++s) {
             const int t = t0 + s;
             float fv = 0.f;  // element tid (< cin0) of frame t
@@ -341,6 +398,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 // round trip brings the value with its tag); thread 0 also ends the launch on a
                 // stop request or after idle_ticks without the frame
                 if (tid < cin0) {
+                    // (the barrier below also publishes end_flag)
                     const gu64* fg = (const gu64*)p.frame_gran + (int64_t)(t & (Q - 1)) * cin0 + tid;
                     const unsigned long long start = __builtin_amdgcn_s_memrealtime();
                     for (;;) {
@@ -371,50 +429,54 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                         __builtin_amdgcn_s_sleep(1);
                     }
                 }
-                __syncthreads();
-                if (end_flag) break;
             }
-            trace_mark(p, wg, s, 0, tid);
+            // the 3-frame input vector (frames t-2, t-1, t; the stream start repeats frame 0):
+            // the next frame writes the other buffer, and a thread reaches the frame after that
+            // only past the next barrier, which every wave passes after its reads of this one
             float* xv = xin + (s & 1) * kPipeExpandK;
+            float nh1 = hp1, nh2 = hp2;
             if (tid < cin0) {
-                const int i = tid;
                 const float v = fv;
-                const float h1 = t == 0 ? v : hist[i];                          // frame t-1
-                const float h2 = t <= 1 ? (t == 0 ? v : h1) : hist[cin0 + i];   // frame t-2
-                xv[i] = h2;
-                xv[cin0 + i] = h1;
-                xv[2 * cin0 + i] = v;
+                const float h1 = t == 0 ? v : hp1;                        // frame t-1
+                const float h2 = t <= 1 ? (t == 0 ? v : h1) : hp2;         // frame t-2
+                xv[tid] = h2;
+                xv[cin0 + tid] = h1;
+                xv[2 * cin0 + tid] = v;
+                nh2 = h1;
+                nh1 = v;
             }
-            for (int i = 3 * cin0 + tid; i < kPipeExpandK; i += kThreads) xv[i] = 0.f;
             __syncthreads();
-            for (int i = tid; i < cin0; i += kThreads) {
-                hist[cin0 + i] = xv[cin0 + i];
-                hist[i] = xv[2 * cin0 + i];
-            }
+            if (p.serve && end_flag) break;  // frame t was never posted: the history stays
+            hp1 = nh1;
+            hp2 = nh2;
+            trace_mark(p, wg, s, 0, tid);
             if (c < c_hi) {
-                float a = 0.f;
+                // four independent chains (two v_pk_fma_f32 chains; a 128-deep dependent chain
+                // is latency-bound)
+                f2 a2[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
-                for (int i = 0; i < kPipeExpandK / 2; ++i) {
-                    a = __builtin_fmaf(lo16<WT>(w[i]), xv[2 * i], a);
-                    a = __builtin_fmaf(hi16<WT>(w[i]), xv[2 * i + 1], a);
-                }
+                for (int i = 0; i < kPipeExpandK / 2; ++i)
+                    a2[i & 1] = __builtin_elementwise_fma(w[i], *(const f2*)(xv + 2 * i), a2[i & 1]);
+                const float a = (a2[0].x + a2[0].y) + (a2[1].x + a2[1].y);
                 float y = a * sc + sh;
                 y = y > 0.f ? y : 0.f;
-                publish(out_edge(0, t) + c, (unsigned)t + 1u, y);
+                publish(out_at(0, t, c), (unsigned)t + 1u, y);
             }
             trace_mark(p, wg, s, 1, tid);
             // the next frame writes the other xin buffer; hist is rewritten only after the
             // next barrier, which every wave passes after its reads of this frame
         }
-        __syncthreads();
-        for (int i = tid; i < 2 * cin0; i += kThreads) gstate[i] = hist[i];
+        if (tid < cin0) {
+            gstate[tid] = hp1;
+            gstate[cin0 + tid] = hp2;
+        }
     } else if (is_k) {
         // ---- block b's k-conv: CWK rows per wave, NT = 3 taps, k-sliced ----
-        uint32_t w[3][CWK][KS / 2];
-        load_rows<WT, 3, CWK, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 3);
+        f2 w[3][CWK][KS / 2];
+        load_rows<WT, 3, CWK, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 3, contig);
         // after rows_sum lane l holds row jr = l >> 4 of the wave's rows: lanes 16 jr lead
         const int jr = lane >> 4, jq = jr < CWK ? jr : CWK - 1;
-        const int cr = c_lo + wid + kWaves * jr;
+        const int cr = row_of<CWK>(c_lo, wid, jr, contig);
         const bool lead = (lane & 15) == 0 && jr < CWK && cr < c_hi;
         const float sc = lead ? scl[cr - c_lo] : 0.f, sh = lead ? scl[kPipeMaxCh + cr - c_lo] : 0.f;
         Pref pf;
@@ -422,8 +484,8 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         for (int s = 0; p.serve || s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
-            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, limit, endw,
-                             &end_flag) &&
+            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, rounds, pause,
+                             limit, endw, &end_flag) &&
                 !end_flag)
                 abort_flag = 1;
             __syncthreads();
@@ -431,21 +493,21 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             if (end_flag) break;
             trace_mark(p, wg, s, 0, tid);
             if (p.serve || s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
-            float xl[KS];
+            f2 xl[KS / 2];
             load_x<KS>(xl, xv, lane);
             float vp[CWK];
-            lane_dots<WT, 3, CWK, KS>(w, xl, 2, vp);
+            lane_dots<3, CWK, KS>(w, xl, 2, vp);
             const float vn = rows_sum<CWK>(vp, lane);  // newest tap, row jr
             const int slot = t & (R - 1);
             if (t == 0) {
                 // every tap reads x(0); outputs 1..2d start from the taps that still reach
                 // before the stream start
                 float v0p[CWK], v1p[CWK];
-                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0p);
-                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1p);
+                lane_dots<3, CWK, KS>(w, xl, 0, v0p);
+                lane_dots<3, CWK, KS>(w, xl, 1, v1p);
                 const float v0 = rows_sum<CWK>(v0p, lane), v1 = rows_sum<CWK>(v1p, lane);
                 const float y = ((v0 + v1) + vn) * sc + sh;
-                if (lead) publish(out_edge(role, t) + cr, (unsigned)t + 1u, y > 0.f ? y : 0.f);
+                if (lead) publish(out_at(role, t, cr), (unsigned)t + 1u, y > 0.f ? y : 0.f);
                 trace_mark(p, wg, s, 1, tid);
                 // ring: all slots zero, then outputs tt = 1..2d from the clamped taps
                 for (int i = lane; i < R * CWK; i += 64) wring[i] = 0.f;
@@ -459,12 +521,12 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 }
             } else {
                 const float y = (wring[slot * CWK + jq] + vn) * sc + sh;
-                if (lead) publish(out_edge(role, t) + cr, (unsigned)t + 1u, y > 0.f ? y : 0.f);
+                if (lead) publish(out_at(role, t, cr), (unsigned)t + 1u, y > 0.f ? y : 0.f);
                 trace_mark(p, wg, s, 1, tid);
                 // the older taps of x(t) feed outputs t + d (tap 1) and t + 2d (tap 0)
                 float v0p[CWK], v1p[CWK];
-                lane_dots<WT, 3, CWK, KS>(w, xl, 1, v1p);
-                lane_dots<WT, 3, CWK, KS>(w, xl, 0, v0p);
+                lane_dots<3, CWK, KS>(w, xl, 1, v1p);
+                lane_dots<3, CWK, KS>(w, xl, 0, v0p);
                 const float v1 = rows_sum<CWK>(v1p, lane), v0 = rows_sum<CWK>(v0p, lane);
                 if (lead) {
                     wring[slot * CWK + jq] = 0.f;
@@ -477,44 +539,44 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         for (int i = tid; i < kWaves * R * CWK; i += kThreads) gstate[i] = ring[i];
     } else {
         // ---- block b's 1x1 conv (+ residual x_b(t)) or the shrink: CWP rows per wave ----
-        uint32_t w[1][CWP][KS / 2];
-        load_rows<WT, 1, CWP, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 1);
+        f2 w[1][CWP][KS / 2];
+        load_rows<WT, 1, CWP, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 1, contig);
         // after rows_sum lane l holds row l >> 3 of the wave's rows: lanes 8 j lead
-        const int cr = c_lo + wid + kWaves * (lane >> 3);
+        const int cr = row_of<CWP>(c_lo, wid, lane >> 3, contig);
         const bool lead = (lane & 7) == 0 && cr < c_hi;
         const float sc = lead ? scl[cr - c_lo] : 0.f, sh = lead ? scl[kPipeMaxCh + cr - c_lo] : 0.f;
         const int nres = is_p ? c_hi - c_lo : 0;
         Pref pf, pr;
-        pref_issue(pr, edge(role - 2, t0) + c_lo, nres, tid);
+        pref_issue(pr, edge(role - 2, t0, c_lo), nres, tid);
         pref_issue(pf, edge(role - 1, t0), C, tid);
         for (int s = 0; p.serve || s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
             float* rv = rbuf + (s & 1) * kPipeMaxCh;
-            bool ok = pref_finish(pr, edge(role - 2, t) + c_lo, nres, (unsigned)t + 1u, rv, &abort_flag, p.fault, tid,
-                                  limit, endw, &end_flag);
+            bool ok = pref_finish(pr, edge(role - 2, t, c_lo), nres, (unsigned)t + 1u, rv, &abort_flag, p.fault, tid,
+                                  rounds, pause, limit, endw, &end_flag);
             if (ok)
-                ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, limit, endw,
-                                 &end_flag);
+                ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, rounds,
+                                 pause, limit, endw, &end_flag);
             if (!ok && !end_flag) abort_flag = 1;
             __syncthreads();
             if (abort_flag) return;
             if (end_flag) break;
             trace_mark(p, wg, s, 0, tid);
             if (p.serve || s + 1 < p.steps) {  // the next frame's loads are in flight during this one
-                pref_issue(pr, edge(role - 2, t + 1) + c_lo, nres, tid);
+                pref_issue(pr, edge(role - 2, t + 1, c_lo), nres, tid);
                 pref_issue(pf, edge(role - 1, t + 1), C, tid);
             }
-            float xl[KS];
+            f2 xl[KS / 2];
             load_x<KS>(xl, xv, lane);
             float vp[CWP];
-            lane_dots<WT, 1, CWP, KS>(w, xl, 0, vp);
+            lane_dots<1, CWP, KS>(w, xl, 0, vp);
             float y = rows_sum<CWP>(vp, lane) * sc + sh;
             if (lead) {
                 if (is_p) {
                     y = y > 0.f ? y : 0.f;
                     y += rv[cr - c_lo];
-                    publish(out_edge(role, t) + cr, (unsigned)t + 1u, y);
+                    publish(out_at(role, t, cr), (unsigned)t + 1u, y);
                 } else if (p.serve) {
                     // host-mapped pose ring: the granule's tag tells the host it is there
                     const unsigned long long g = ((unsigned long long)((unsigned)t + 1u) << 32) | __float_as_uint(y);

@@ -934,12 +934,15 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     const int nout = h->layers[nl - 1].cout;
     const int n_e = (C + 255) / 256, n_s = (nout + 15) / 16;
     const int per_block = (cus - n_e - n_s) / nb;
-    const int min_k = (C + 8 * kPipeCwK - 1) / (8 * kPipeCwK), min_p = (C + 8 * kPipeCwP - 1) / (8 * kPipeCwP);
+    // channels are split over a role's workgroups in units of 8 (stream_pipe.hip); a workgroup
+    // holds at most 8 waves x CW rows = CW units
+    const int units = (C + 7) / 8;
+    const int min_k = (units + kPipeCwK - 1) / kPipeCwK, min_p = (units + kPipeCwP - 1) / kPipeCwP;
     int n_p = std::max(min_p, per_block / 4);
     int n_k = per_block - n_p;
     n_k = std::min(n_k, std::max(min_k, C / 8));   // small models: fewer, fuller workgroups
     n_p = std::min(n_p, std::max(min_p, C / 16));
-    if (n_k < min_k || (nout + n_s - 1) / n_s > 8 * kPipeCwP) return false;
+    if (n_k < min_k || ((nout + 7) / 8 + n_s - 1) / n_s > kPipeCwP) return false;
     StreamPipeParams& p = st->pipe_p;
     p = StreamPipeParams{};
     p.nl = nl;
@@ -974,7 +977,18 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     if (lds > 160 * 1024 || stream_pipe_prepare(wt, C, lds) != hipSuccess) return false;
     st->pipe_lds = lds;
     p.state_stride = std::max(8 * max_ring * kPipeCwK, 2 * p.cin0);
-    st->pipe_gran_bytes = (size_t)kQueue * (2 * nb + 1) * C * 8;
+    // hand-off layout and polling (defaults measured in round 3, tools/stream_latency.py)
+    p.chunk_stride = 64;
+    p.poll_rounds = 1;
+    p.poll_pause = 1;
+    // contiguous rows: a wave's outputs are neighbouring granules stored by one instruction
+    // (strided rows put 8 waves' stores into every 64-byte line: hand-offs 0.4-1.0 us slower)
+    p.row_contig = 1;
+    if (const char* e = getenv("VP3D_STREAM_ROWS")) p.row_contig = strcmp(e, "strided") != 0;
+    if (const char* e = getenv("VP3D_STREAM_CHUNK_STRIDE")) p.chunk_stride = std::max(64, atoi(e));
+    if (const char* e = getenv("VP3D_STREAM_POLL_ROUNDS")) p.poll_rounds = std::min(2, std::max(1, atoi(e)));
+    if (const char* e = getenv("VP3D_STREAM_POLL_PAUSE")) p.poll_pause = std::min(64, std::max(0, atoi(e)));
+    st->pipe_gran_bytes = (size_t)kQueue * (2 * nb + 1) * (C / 64) * p.chunk_stride * 8;
     if (hipMalloc(&st->pipe_gran, st->pipe_gran_bytes) != hipSuccess) return false;
     if (hipMalloc(&st->pipe_state, (size_t)g * p.state_stride * 4) != hipSuccess) {
         hipFree(st->pipe_gran);
@@ -993,8 +1007,9 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     p.state = st->pipe_state;
     if (const char* e = getenv("VP3D_STREAM_TRACE")) {
         const int n = atoi(e);
-        if (n > 0 && hipMalloc(&st->pipe_trace, (size_t)g * n * 16) == hipSuccess) {
-            hipMemset(st->pipe_trace, 0, (size_t)g * n * 16);
+        const size_t tb = (size_t)g * n * kStreamTraceSlots * 8;
+        if (n > 0 && hipMalloc(&st->pipe_trace, tb) == hipSuccess) {
+            hipMemset(st->pipe_trace, 0, tb);
             p.trace = st->pipe_trace;
             p.trace_frames = n;
         }
@@ -1344,6 +1359,17 @@ int vp3d_stream_serve_wait(vp3d_stream* st, int64_t frame_index, float* pose, do
     return VP3D_OK;
 }
 
+int vp3d_stream_serve_step(vp3d_stream* st, const float* frame, float* pose, double timeout_ms, double* latency_us) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t t = 0;
+    int rc = vp3d_stream_serve_post(st, frame, &t);
+    if (rc != VP3D_OK) return rc;
+    rc = vp3d_stream_serve_wait(st, t, pose, timeout_ms);
+    if (latency_us)
+        *latency_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
 int vp3d_stream_serve_end(vp3d_stream* st, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     if (!st->serving) return VP3D_OK;
@@ -1366,7 +1392,7 @@ int vp3d_stream_trace(vp3d_stream* st, uint64_t* out, int64_t capacity, int32_t*
     *frames = p.trace_frames;
     if (role_first_wg)
         for (int l = 0; l <= p.nl; ++l) role_first_wg[l] = p.cu0[l];
-    const int64_t need = (int64_t)p.cu0[p.nl] * p.trace_frames * 2;
+    const int64_t need = (int64_t)p.cu0[p.nl] * p.trace_frames * kStreamTraceSlots;
     if (!out) return VP3D_OK;
     if (capacity < need) return fail(VP3D_ERR_ARG, "trace buffer too small");
     HIP_TRY(hipDeviceSynchronize());

@@ -52,7 +52,7 @@ EXPORTS = [
     "vp3d_stream_frames_seen", "vp3d_stream_graph_capture", "vp3d_stream_graph_launch",
     "vp3d_stream_destroy", "vp3d_stream_persistent", "vp3d_stream_mode", "vp3d_stream_status",
     "vp3d_stream_serve_begin", "vp3d_stream_serve_post", "vp3d_stream_serve_wait", "vp3d_stream_serve_end",
-    "vp3d_stream_trace",
+    "vp3d_stream_trace", "vp3d_stream_serve_step",
     "vp3d_trainer_create", "vp3d_trainer_destroy", "vp3d_train_forward", "vp3d_train_backward",
     "vp3d_train_dropout_mask", "vp3d_train_relu_mask", "vp3d_train_layer_rows", "vp3d_adam_step", "vp3d_mpjpe_backward",
     "vp3d_seq_weight_count", "vp3d_seq_create", "vp3d_seq_destroy", "vp3d_seq_forward",
@@ -148,6 +148,7 @@ _SIGNATURES = {
     "vp3d_stream_serve_wait": (_int, [_vp, _i64, _vp, ctypes.c_double]),
     "vp3d_stream_serve_end": (_int, [_vp, _vp]),
     "vp3d_stream_trace": (_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp]),
+    "vp3d_stream_serve_step": (_int, [_vp, _vp, _vp, ctypes.c_double, _vp]),
     "vp3d_trainer_create": (_int, [ctypes.POINTER(vp3d_cfg), ctypes.POINTER(_vp)]),
     "vp3d_trainer_destroy": (_int, [_vp]),
     "vp3d_train_forward": (_int, [_vp, ctypes.POINTER(_vp), _int, _vp, _int, _int, ctypes.c_float,

@@ -85,15 +85,16 @@ class CausalStream:
     def trace(self):
         """Per-frame device clocks of the layer-pipelined launch (VP3D_STREAM_TRACE=n set
         before the stream was created): returns (clocks, role_first_wg) with clocks of shape
-        (workgroups, n, 2) -- [..., 0] input complete, [..., 1] first output stored, 100 MHz
-        ticks, 0 = not recorded -- for the first n frames of the last launch, then clears them."""
+        (workgroups, n, 11) -- [..., 0] input complete, [..., 1 + w] wave w's first output
+        stored, 100 MHz ticks, 0 = not recorded; [..., 9], [..., 10] the shader clock counter
+        at [..., 0] and [..., 1] -- for the first n frames of the last launch, then clears them."""
         roles, frames = ctypes.c_int32(), ctypes.c_int32()
         N.check(self._lib.vp3d_stream_trace(self._s, None, 0, None, ctypes.byref(roles), ctypes.byref(frames)),
                 "vp3d_stream_trace")
         first = np.zeros(roles.value + 1, np.int32)
         N.check(self._lib.vp3d_stream_trace(self._s, None, 0, first.ctypes.data, ctypes.byref(roles),
                                             ctypes.byref(frames)), "vp3d_stream_trace")
-        out = np.zeros((int(first[-1]), frames.value, 2), np.uint64)
+        out = np.zeros((int(first[-1]), frames.value, 11), np.uint64)
         with torch.cuda.device(self.device):
             N.check(self._lib.vp3d_stream_trace(self._s, out.ctypes.data, out.size, first.ctypes.data,
                                                 ctypes.byref(roles), ctypes.byref(frames)), "vp3d_stream_trace")
@@ -161,8 +162,17 @@ class Serving:
                 "vp3d_stream_serve_wait")
         return out.reshape(-1, 3)
 
-    def step(self, frame) -> np.ndarray:
-        return self.wait(self.post(frame))
+    def step(self, frame, timeout_ms: float = 1000.0) -> np.ndarray:
+        """post + wait in one library call; the pose (J_out, 3).  `last_latency_us` = the
+        library's own wall time for it (post start -> pose copied out, no Python overhead)."""
+        f = np.ascontiguousarray(np.asarray(frame, dtype=np.float32)).reshape(-1)
+        assert f.size == self.st.n_in
+        out = np.empty(self.st.n_out, dtype=np.float32)
+        lat = ctypes.c_double()
+        N.check(self.st._lib.vp3d_stream_serve_step(self.st._s, f.ctypes.data, out.ctypes.data, float(timeout_ms),
+                                                    ctypes.byref(lat)), "vp3d_stream_serve_step")
+        self.last_latency_us = lat.value
+        return out.reshape(-1, 3)
 
     def __exit__(self, *exc):
         with torch.cuda.device(self.st.device):

@@ -205,12 +205,16 @@ int vp3d_stream_serve_post(vp3d_stream* s, const float* frame, int64_t* frame_in
 /* Wait (spinning on host memory, at most timeout_ms) until frame `frame_index` is done and
  * copy its pose (host f32, J_out * 3) out.  VP3D_ERR_STATE on timeout or stream fault. */
 int vp3d_stream_serve_wait(vp3d_stream* s, int64_t frame_index, float* pose, double timeout_ms);
+/* post + wait in one call (one frame in flight); *latency_us (or NULL) = host wall time from
+ * the start of the post to the pose copied out. */
+int vp3d_stream_serve_step(vp3d_stream* s, const float* frame, float* pose, double timeout_ms, double* latency_us);
 /* Stop serving: the launch finishes the posted frames and exits; synchronises `stream`. */
 int vp3d_stream_serve_end(vp3d_stream* s, void* stream);
 /* Diagnostics of the layer-pipelined form (no reference counterpart): with VP3D_STREAM_TRACE=n
  * set at vp3d_stream_create, every workgroup records the 100 MHz device clock when the input of
- * each of the first n frames of a launch is complete and after its first output store.  Copies
- * workgroups x n x 2 clocks to `out` (NULL: sizes only) and clears them; role_first_wg (n_roles
+ * each of the first n frames of a launch is complete and, per wave, after the wave's first
+ * output store.  Copies workgroups x n x 11 clocks ([0] input complete, [1 + w] wave w stored;
+ * [9], [10]: the shader clock counter at [0] and [1]) to `out` (NULL: sizes only) and clears them; role_first_wg (n_roles
  * + 1 entries, or NULL) = the first workgroup of each layer role (expand, k / 1x1 per block,
  * shrink).  Synchronises the device. */
 int vp3d_stream_trace(vp3d_stream* s, uint64_t* out, int64_t capacity, int32_t* role_first_wg, int32_t* n_roles,

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-3 profile session (one gpurun call): rocprofv3 kernel traces of the headline bench
+# Round-3 profile session (one gpurun call): the default bench line (as the driver runs it),
+# rocprofv3 kernel traces of the headline bench
 # (bf16), the fp32 and f16x3 legs alone, and the config-5 stream; PMC passes (counters
 # only, one pass each): FETCH_SIZE / WRITE_SIZE for bf16 and f16x3, MFMA-busy and
 # instruction-wait cycles for bf16; FETCH / WRITE for the stream.
@@ -16,6 +17,7 @@ run() {  # name, timeout, command...
   echo "$name rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/$name.log; exit $rc; fi
 }
+run bench_default 600 python bench.py
 B="python bench.py --steps 5 --warmup 2 --cpu-seconds 0 --parity-windows 4 --no-extras"
 run trace_bf16 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_bf16 -o run --output-format csv -- $B
 run trace_fp32 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_fp32 -o run --output-format csv -- $B --dtype fp32

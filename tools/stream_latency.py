@@ -40,12 +40,13 @@ def main():
     st = CausalStream(model.native_lifter(dev), "fp16")
     assert st.mode == "pipe", st.mode
     frames = np.random.RandomState(0).uniform(-1, 1, (a.frames, 17 * 2)).astype(np.float32)
-    wall = []
+    wall, native = [], []
     with st.serve(idle_ms=200.0) as sv:
         for i in range(a.frames):
             t0 = time.perf_counter_ns()
             sv.step(frames[i])
             wall.append((time.perf_counter_ns() - t0) * 1e-3)
+            native.append(sv.last_latency_us)
     clk, first = st.trace()
     st.close()
     names = ["expand"] + [f"{k}{b}" for b in range(1, (len(first) - 3) // 2 + 1) for k in ("k", "p")] + ["shrink"]
@@ -55,21 +56,29 @@ def main():
         if not t_exp.all():
             continue
         base = int(t_exp.min())
-        r = {"wall_us": wall[s]}
+        r = {"wall_us": wall[s], "native_us": native[s]}
         for i, n in enumerate(names):
-            c = clk[first[i]:first[i + 1], s]
-            if not c.all():
+            c = clk[first[i]:first[i + 1], s].astype(np.int64)
+            if not c[:, 0].all():
                 break
-            r[n] = ((int(c[:, 0].max()) - base) / 100.0, (int(c[:, 1].max()) - base) / 100.0,
-                    (int(c[:, 0].min()) - base) / 100.0, (int(c[:, 1].min()) - base) / 100.0)
+            outs = c[:, 1:9]
+            outs = outs[outs > 0]  # waves that recorded a store
+            # (last input, last store of any wave, first input, first store)
+            r[n] = ((int(c[:, 0].max()) - base) / 100.0, (int(outs.max()) - base) / 100.0,
+                    (int(c[:, 0].min()) - base) / 100.0, (int(outs.min()) - base) / 100.0)
+        # shader clock of wave 0 between its input and output marks, every workgroup
+        cl = clk[:, s].astype(np.int64)
+        ok = (cl[:, 1] > cl[:, 0]) & (cl[:, 10] > cl[:, 9])
+        if ok.any():
+            r["sclk_mhz"] = float(np.median((cl[ok, 10] - cl[ok, 9]) / ((cl[ok, 1] - cl[ok, 0]) / 100.0)))
         rows.append(r)
     skip = min(8, len(rows) // 2)  # first frames: weights to VGPRs, clocks up
     steady = rows[skip:]
-    med = {"wall_us": float(np.median([r["wall_us"] for r in steady]))}
+    med = {k: float(np.median([r[k] for r in steady])) for k in ("wall_us", "native_us")}
     for n in names:
         if all(n in r for r in steady):
             med[n] = tuple(float(np.median([r[n][k] for r in steady])) for k in range(4))
-    print("role: input complete / first output stored by the LAST (first) workgroup of the role, us after the "
+    print("role: input complete / output stored by the LAST (first) workgroup or wave of the role, us after the "
           f"first expand workgroup had the frame (median of {len(steady)} frames)")
     prev = 0.0
     for n in names:
@@ -78,7 +87,12 @@ def main():
             print(f"  {n:7s} in {i:7.2f} ({i0:6.2f})  out {o:7.2f} ({o0:6.2f})   "
                   f"(hand-off {i - prev:5.2f}, compute {o - i:5.2f})")
             prev = o
-    print(f"  host wall (post -> pose in host memory): {med['wall_us']:.2f} us")
+    sc = [r["sclk_mhz"] for r in steady if "sclk_mhz" in r]
+    if sc:
+        med["sclk_mhz"] = float(np.median(sc))
+        print(f"  shader clock while a workgroup computes a frame: {med['sclk_mhz']:.0f} MHz (s_memtime / s_memrealtime)")
+    print(f"  host wall (post -> pose in host memory): library {med['native_us']:.2f} us, "
+          f"with the Python call {med['wall_us']:.2f} us")
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"median": med, "frames": rows, "names": names, "role_first_wg": first.tolist()}, f, indent=1)

@@ -42,6 +42,8 @@ def forwards(rows, B):
     # the fused expand kernel runs 256 rows per workgroup (RB = 4) or 128 (RB = 2, the
     # camera concat): grid in threads = workgroups x 256
     expand_grids = {((B * 81 + 255) // 256) * 256, ((B * 81 + 127) // 128) * 256}
+    # other expand forms (f16x3: two workgroups per CU): the largest expand grid in the trace
+    expand_grids.add(max((g for n, g, _ in rows.values() if "expand_gemm" in n), default=0))
     i = 0
     while i < len(ids):
         name, grid, _ = rows[ids[i]]
