@@ -181,7 +181,7 @@ struct StreamPipeParams {
     unsigned* arrivals;                    // end-of-launch arrival counter (zero between launches)
     unsigned long long* gran;              // [queue][2nb+1 edges][C / 64 chunks x chunk_stride] granules
     int chunk_stride;                      // granules between the 64-granule chunks of an edge (>= 64)
-    int poll_rounds, poll_pause;           // poll rounds in flight (1, 2); s_sleep 1 pauses between rounds
+    int poll_pause;                        // s_sleep 1 pauses between polls of a hand-off
     int row_contig;                        // a wave's rows contiguous (1) or kWaves apart (0)
     StreamFault fault;                     // sticky timeout word
     float* state;                          // [workgroups][state_stride]: k-conv rings / expand history

@@ -160,11 +160,13 @@ __device__ __forceinline__ void poll_pause(int n) {
 // true once every granule carried `tag`; false on timeout (sets the fault words) or when
 // another wave aborted, or -- serve form -- once the launch ended before frame tag - 1
 // (*end < tag: that frame is never produced; *ended is then set).
-// rounds = 1: one poll of the missing granules in flight, waited for before the next;
-// rounds = 2: two rounds in flight (r and q alternate, each re-issued before the other is
-// checked).  `pause` x s_sleep 1 between rounds.
+// One poll of the missing granules in flight, waited for before the next, `pause` x
+// s_sleep 1 between polls.  (Two rounds in flight measured slower: 0.5-0.7 us more per
+// hand-off, tools/stream_latency.py; and a round still in flight when the function returns
+// makes the compiler drain vmcnt before the next reuse of its registers -- which was the
+// prefetch of the next frame.)
 __device__ bool pref_finish(Pref& r, const EdgeRef& e, int n, unsigned tag, float* x, volatile int* abort_flag,
-                            const StreamFault& f, int tid, int rounds, int pause, unsigned long long limit = 0,
+                            const StreamFault& f, int tid, int pause, unsigned long long limit = 0,
                             const unsigned* end = nullptr, volatile int* ended = nullptr) {
     if (limit == 0) limit = f.spin_ticks;
     unsigned pending = 0;
@@ -192,22 +194,8 @@ __device__ bool pref_finish(Pref& r, const EdgeRef& e, int n, unsigned tag, floa
         }
         return 0;
     };
-    if (rounds < 2) {
-        for (;;) {
-            pref_issue(r, e, n, tid, pending);
-            if (pref_check(r, pending, tag, x, tid)) return true;
-            if (give_up()) return false;
-            poll_pause(pause);
-        }
-    }
-    Pref q;
-    pref_issue(q, e, n, tid, pending);
     for (;;) {
         pref_issue(r, e, n, tid, pending);
-        if (pref_check(q, pending, tag, x, tid)) return true;
-        if (give_up()) return false;
-        poll_pause(pause);
-        pref_issue(q, e, n, tid, pending);
         if (pref_check(r, pending, tag, x, tid)) return true;
         if (give_up()) return false;
         poll_pause(pause);
@@ -366,7 +354,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     auto out_at = [&](int e, int t, int c) {
         return (gu64*)p.gran + ((int64_t)(t & (Q - 1)) * nE + e) * edge_len + (c >> 6) * cs + (c & 63);
     };
-    const int rounds = p.poll_rounds, pause = p.poll_pause;
+    const int pause = p.poll_pause;
 
     if (is_expand) {
         // ---- lane per channel: row c = c_lo + 64 wid + lane, Kp0 (<= 128) 16-bit weights ----
@@ -484,7 +472,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         for (int s = 0; p.serve || s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
-            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, rounds, pause,
+            if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, pause,
                              limit, endw, &end_flag) &&
                 !end_flag)
                 abort_flag = 1;
@@ -554,9 +542,9 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             float* xv = xbuf + (s & 1) * C;
             float* rv = rbuf + (s & 1) * kPipeMaxCh;
             bool ok = pref_finish(pr, edge(role - 2, t, c_lo), nres, (unsigned)t + 1u, rv, &abort_flag, p.fault, tid,
-                                  rounds, pause, limit, endw, &end_flag);
+                                  pause, limit, endw, &end_flag);
             if (ok)
-                ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, rounds,
+                ok = pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid,
                                  pause, limit, endw, &end_flag);
             if (!ok && !end_flag) abort_flag = 1;
             __syncthreads();

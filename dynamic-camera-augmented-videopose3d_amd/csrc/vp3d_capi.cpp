@@ -979,14 +979,12 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     p.state_stride = std::max(8 * max_ring * kPipeCwK, 2 * p.cin0);
     // hand-off layout and polling (defaults measured in round 3, tools/stream_latency.py)
     p.chunk_stride = 64;
-    p.poll_rounds = 1;
     p.poll_pause = 1;
     // contiguous rows: a wave's outputs are neighbouring granules stored by one instruction
     // (strided rows put 8 waves' stores into every 64-byte line: hand-offs 0.4-1.0 us slower)
     p.row_contig = 1;
     if (const char* e = getenv("VP3D_STREAM_ROWS")) p.row_contig = strcmp(e, "strided") != 0;
     if (const char* e = getenv("VP3D_STREAM_CHUNK_STRIDE")) p.chunk_stride = std::max(64, atoi(e));
-    if (const char* e = getenv("VP3D_STREAM_POLL_ROUNDS")) p.poll_rounds = std::min(2, std::max(1, atoi(e)));
     if (const char* e = getenv("VP3D_STREAM_POLL_PAUSE")) p.poll_pause = std::min(64, std::max(0, atoi(e)));
     st->pipe_gran_bytes = (size_t)kQueue * (2 * nb + 1) * (C / 64) * p.chunk_stride * 8;
     if (hipMalloc(&st->pipe_gran, st->pipe_gran_bytes) != hipSuccess) return false;
