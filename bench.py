@@ -100,6 +100,17 @@ def synth_windows(B, T, jin, seed, device):
     return (base + torch.cumsum(steps, dim=1)).contiguous()
 
 
+def stream_traffic(mode):
+    """HBM bytes per pipelined step (graph of 64) of the stream kernel from the committed PMC
+    summary (profiles/r03prof_stream_traffic.json: FETCH_SIZE x 2 + WRITE_SIZE per graph
+    launch / 64: the weights once per launch plus the hand-off polls), or None."""
+    tfile = os.path.join(REPO, "profiles", "r03prof_stream_traffic.json")
+    if mode != "pipe" or not os.path.exists(tfile):
+        return None
+    with open(tfile) as f:
+        return json.load(f).get("per_step_in_graph_bytes")
+
+
 def stream_main(args, world, rank, dev):
     """Config 5: causal TemporalModel, one frame in / one pose out per step.  16-bit
     weights: a graph of Q steps is ONE persistent launch -- by default the layer-pipelined
@@ -227,7 +238,8 @@ def stream_main(args, world, rank, dev):
                      "unit": "TFLOP/s" if mode != "launches" else "GB/s",
                      "frac": round(step_flop / step_s / 1e12 / 157.3, 4) if mode != "launches"
                      else round(achieved / 8000.0, 4),
-                     "traffic": None, "flop_per_step": step_flop, "avg_step_us": round(step_s * 1e6, 3),
+                     "traffic": stream_traffic(mode), "flop_per_step": step_flop,
+                     "avg_step_us": round(step_s * 1e6, 3),
                      "note": ("achieved = the step's algorithmic FLOP (2 x MACs of the 10 convs) / the pipelined "
                               "step time (frames of a 64-step graph flowing through the layer groups); peak = "
                               "the f32 vector peak (157.3 TF spec; the unpacked v_fma_mix_f32 the kernel issues "
@@ -745,11 +757,15 @@ def windows_main(args, world, rank, dev):
               f"{dtype}_mpjpe_delta_mm": abs(mp(y_fast) - mp(ref)) * 1e3,
               f"{dtype}_max_coord_delta_mm": float(np.abs(y_fast - ref).max()) * 1e3}
 
-    traffic = None
-    tfile = os.path.join(REPO, "profiles", f"traffic_{dtype}_b{B}{'_traj' if traj else ''}.json")
-    if os.path.exists(tfile):
-        with open(tfile) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    def committed_traffic(dt):
+        """HBM bytes per launch of the dominant kernel from the committed PMC summary
+        (tools/traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE passes), or None."""
+        tfile = os.path.join(REPO, "profiles", f"traffic_{dt}_b{B}{'_traj' if traj else ''}.json")
+        if os.path.exists(tfile):
+            with open(tfile) as f:
+                return json.load(f).get("hbm_bytes_per_launch")
+        return None
+    traffic = committed_traffic(dtype)
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
@@ -789,7 +805,7 @@ def windows_main(args, world, rank, dev):
                 yas = ya[idx].cpu().numpy()
                 out[dt_acc] = {"value": round(G * ksteps / dta, 2), "unit": "poses/s", "steps": ksteps,
                                "ms_per_step": round(dta / ksteps * 1e3, 4),
-                               "roofline": roofline_of(doma, PEAK_TFLOPS[dt_acc]),
+                               "roofline": roofline_of(doma, PEAK_TFLOPS[dt_acc], committed_traffic(dt_acc)),
                                "per_layer_ms": pla,
                                "mpjpe_delta_mm": abs(mp(yas) - mp(ref)) * 1e3,
                                "max_coord_delta_mm": float(np.abs(yas - ref).max()) * 1e3}

@@ -77,11 +77,15 @@ def per_layer(trace, B):
     # the expand grid of the largest forward in the trace (the bench's batch; the 16-bit
     # expand's grid depends on its row-block form, so it is not derived from B)
     eg = max((r[2] for r in rows if "expand_gemm" in r[1]), default=0)
+    starts = "expand_gemm"
+    if eg == 0:  # the fp32 path: the expand is the largest conv_gemm_f32 launch
+        eg = max((r[2] for r in rows if "conv_gemm_f32" in r[1]), default=0)
+        starts = "conv_gemm_f32"
     agg = defaultdict(list)
     names = {}
     i = 0
     while i < len(rows):
-        if "expand_gemm" in rows[i][1] and rows[i][2] == eg:
+        if starts in rows[i][1] and rows[i][2] == eg:
             seq = [rows[i]]
             j = i + 1
             while j < len(rows) and len(seq) < len(layers):
