@@ -335,6 +335,7 @@ int gemm_8p_mode() {
     if (strcmp(e, "8p") == 0) return 2;
     if (strcmp(e, "q64") == 0) return 3;
     if (strcmp(e, "h16") == 0) return 4;  // the 128x128 kernel everywhere (measurement)
+    if (strcmp(e, "a4") == 0) return 5;   // the one-wave-per-SIMD AGPR kernel where eligible
     return strcmp(e, "big") == 0 ? 0 : 1;
 }
 bool gemm_8p_env(const ConvGemmParams& p) {
@@ -448,6 +449,8 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
         return hipGetLastError();
     }
     const int gm = gemm_8p_mode();
+    if (gm == 5 && p.dil == 1 && conv_gemm_a4_eligible(p, a_type, out_type, compute))
+        return launch_conv_gemm_a4(p, compute, stream);
     if ((gm == 3 || (gm == 1 && p.dil == 1)) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_q64_eligible(p, a_type, out_type, compute))
         return launch_conv_gemm_q64(p, compute, stream);

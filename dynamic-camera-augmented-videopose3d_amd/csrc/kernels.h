@@ -53,6 +53,10 @@ hipError_t launch_conv_gemm_8p(const ConvGemmParams& p, Act compute, hipStream_t
 // 64-deep K-tiles staged as whole 128-byte lines, quadrant phases (conv_gemm_q64.hip).
 bool conv_gemm_q64_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_t stream);
+// One wave per SIMD, 128 x 128 wave tiles, accumulators in named AGPRs (conv_gemm_a4.hip);
+// same contract as q64.
+bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
+hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream);
 // Split-fp16 mode of conv_gemm_q64 (VP3D_DTYPE_F16X3): A / W / residual rows of f16 halves,
 // each 32-wide K group [hi(32) | lo(32)] (Ktap, Kp, lda, ldr in halves); output split
 // (ldy halves) or, out_f32, f32 rows (ldy floats).  N % 64 == 0, N <= 1024.

@@ -129,6 +129,28 @@ def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
     _check(y, ref, gt, "bf16")
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_gemm_a4_bit_identical_to_q64(dtype, monkeypatch):
+    """The one-wave-per-SIMD AGPR kernel (conv_gemm_a4.hip) sums every output in q64's K
+    order (two 16x16x32 MFMAs per 64-deep K-tile, K-tiles in order), so every strided
+    k3 conv and 1x1 conv + residual of Optimized1f gives the same bits on either kernel;
+    B = 2050 leaves every layer a ragged last row tile (block 1: 55,350 rows)."""
+    model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
+    x = synth.normalized_windows(1, "x2050_243", 2050, 243)
+    model.cuda().set_compute_dtype(dtype)
+    xd = torch.from_numpy(x).cuda()
+    ys = {}
+    for gemm in ("q64", "a4"):
+        monkeypatch.setenv("VP3D_GEMM", gemm)
+        with torch.no_grad():
+            ys[gemm] = model(xd).cpu().numpy()
+    assert np.isfinite(ys["a4"]).all()
+    assert np.array_equal(ys["a4"], ys["q64"]), np.abs(ys["a4"] - ys["q64"]).max()
+    ref = lifter_forward(sd, x, [3, 3, 3, 3, 3], causal=False, strided=True, dense=False).numpy()
+    gt = synth.gt_poses(3, "gt", 2050, 17).reshape(ref.shape)
+    _check(ys["a4"], ref, gt, dtype)
+
+
 def test_dilated_long_seq_bf16():
     # one long sequence: every block layer has >= 384 output tiles, so the dilated
     # taps (row offsets 0, d, 2d) and the residual slice run on the LDS-ring kernel

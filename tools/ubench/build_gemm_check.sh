@@ -11,5 +11,5 @@ FL="-x hip --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I ../../inclu
 hipcc $FL -c gemm_check.hip -o /tmp/gemm_check.o
 hipcc $FL -DVP3D_ABLATION -c $CS/conv_gemm_8p.hip -o /tmp/conv_gemm_8p_abl.o
 hipcc $FL -DVP3D_ABLATION -c $CS/conv_gemm_q64.hip -o /tmp/conv_gemm_q64_abl.o
-hipcc --offload-arch=gfx950 -o gemm_check /tmp/gemm_check.o $B/conv_gemm.hip.o $B/conv_gemm_big.hip.o \
+hipcc --offload-arch=gfx950 -o gemm_check /tmp/gemm_check.o $B/conv_gemm.hip.o $B/conv_gemm_big.hip.o $B/conv_gemm_a4.hip.o \
   /tmp/conv_gemm_q64_abl.o /tmp/conv_gemm_8p_abl.o

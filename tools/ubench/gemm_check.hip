@@ -1,6 +1,6 @@
 // Conv-GEMM kernel check + timing harness (tool, not product).
 //
-//   gemm_check <kernel: 8p|q64|big|h16> M N K [dil taps residual]
+//   gemm_check <kernel: 8p|q64|a4|big|h16> M N K [dil taps residual]
 //
 // Runs one of the library's conv-GEMM launchers on random 16-bit data and compares
 // it with a naive f32 reference kernel (same bf16 inputs, f32 accumulate): prints
@@ -44,7 +44,7 @@ static float frand(unsigned& s) {
 
 int main(int argc, char** argv) {
     if (argc < 5) {
-        printf("usage: gemm_check 8p|q64|big|h16 M N Cin [dil taps residual]\n");
+        printf("usage: gemm_check 8p|q64|a4|big|h16 M N Cin [dil taps residual]\n");
         return 2;
     }
     const char* kern = argv[1];
@@ -95,6 +95,7 @@ int main(int argc, char** argv) {
         if (!strcmp(kern, "big")) return launch_conv_gemm_big(p, Act::BF16, Act::BF16, 0);
         if (!strcmp(kern, "8p")) return launch_conv_gemm_8p(p, Act::BF16, 0);
         if (!strcmp(kern, "q64")) return launch_conv_gemm_q64(p, Act::BF16, 0);
+        if (!strcmp(kern, "a4")) return launch_conv_gemm_a4(p, Act::BF16, 0);
         return launch_conv_gemm(p, Act::BF16, Act::BF16, Act::BF16, 0);
     };
     hipError_t e = launch();
