@@ -28,6 +28,11 @@
 //            by this wave), barrier
 //   phase B: 64 MFMAs on set 1, reads of set 0 (k 0..31 of t + 1) and this wave's 16 DMA
 //            pieces of tile t + 2 into buffer t & 1, which every wave has finished reading
+// (reads and DMA pieces one per two MFMAs).  Measured (MI355X, random bf16, block-1 shapes at
+// B = 8192, tools/ubench/gemm_check): k3 1.18 ms vs q64 1.29 ms, 1x1 + residual 0.62-0.63 vs
+// 0.66-0.69; MFMA pipes busy 0.68 of the cycles vs 0.57, at a lower clock (1.68 vs 1.81 GHz:
+// the chip holds its power); ablations: without the loop DMA 1.00 ms, without the fragment
+// reads 1.11, without both 0.90.
 // Epilogue: the accumulators copied to VGPRs 128 at a time, gemm::epilogue_tp per 64
 // channels (BN/ReLU, residual, 16-byte stores), as q64.
 #include <cstdlib>
@@ -51,6 +56,7 @@ constexpr int GMAXN = 1024;
 // s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
 constexpr int kLgkm0 = 0xC07F;     // lgkmcnt(0)
 constexpr int kVm0Lgkm0 = 0x0070;  // vmcnt(0) lgkmcnt(0)
+constexpr int kVm16Lgkm0 = 0x4070; // vmcnt(16) lgkmcnt(0)
 
 template <typename F, int... Is>
 __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
@@ -101,7 +107,7 @@ __device__ __forceinline__ float aread() {
         A4_C10(14), A4_C10(15), A4_C10(16), A4_C10(17), A4_C10(18), A4_C10(19), A4_C10(20), A4_C10(21),          \
         A4_C10(22), A4_C10(23), A4_C10(24), "a250", "a251", "a252", "a253", "a254", "a255"
 
-template <typename CT, bool BUF>
+template <typename CT, int ABL>
 __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     // the accumulator file is this kernel's own from here on (see the header)
     asm volatile("" ::: A4_ALL_AGPRS);
@@ -133,11 +139,10 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     // pieces of a wave share the parity of q (= that of w): one swizzled chunk each ----
     const int prow = lane >> 3;
     const int lc = (lane & 7) ^ (((wid & 1) * 4 + (prow >> 1)) & 7);
-    // BUF: buffer_load ... lds through per-tile resources (32-bit lane offsets fixed for the
-    // launch, the tile's k offset in soffset: no per-piece address arithmetic); otherwise
-    // global_load_lds from 64-bit lane pointers
-    const CT* pa[8];
-    const CT* pw[8];
+    // LDS-DMA as buffer_load ... lds through per-tile resources: 32-bit lane offsets fixed
+    // for the launch, the tile's k offset in soffset, so no per-piece address arithmetic
+    // (global_load_lds from 64-bit lane pointers measured 2 % slower: block-1 k3 shape,
+    // B = 8192, 1.251-1.262 vs 1.231-1.237 ms)
     uint32_t va[8], vw[8];
     const int srow0 = src_row(p, m0);  // m0 < M; wave-uniform
     const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc((const CT*)p.A + (int64_t)srow0 * p.lda, 0x7FFFFFFFu);
@@ -146,14 +151,33 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     for (int i = 0; i < 8; ++i) {
         int m = m0 + 8 * (wid + 4 * i) + prow;
         m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
-        if constexpr (BUF) {
-            va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lc * 8) * (int)sizeof(CT));
-            vw[i] = (uint32_t)(((8 * (wid + 4 * i) + prow) * p.Kp + lc * 8) * (int)sizeof(CT));
-        } else {
-            pa[i] = (const CT*)p.A + (int64_t)src_row(p, m) * p.lda + lc * 8;
-            pw[i] = (const CT*)p.W + (int64_t)(n0 + 8 * (wid + 4 * i) + prow) * p.Kp + lc * 8;  // W rows padded to 256
-        }
+        va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lc * 8) * (int)sizeof(CT));
+        vw[i] = (uint32_t)(((8 * (wid + 4 * i) + prow) * p.Kp + lc * 8) * (int)sizeof(CT));  // W rows padded to 256
     }
+    // 1x1 convs (residual): the tile's residual rows land in LDS by LDS-DMA during the last
+    // two K-tiles, into the operand buffers those no longer need -- part h (the channel half
+    // h of both wave columns: 256 rows x 2 x 128 B = 64 KiB) in phase B of tile nk - 2 + h,
+    // in the DMA slots; rows at 128-byte pitch with the operands' chunk swizzle -- so the
+    // epilogue reads them from LDS instead of waiting on global loads row block by row block
+    const int nk = p.Kp / GK;  // >= 1
+    const bool lres = p.R != nullptr && nk >= 3;
+    uint32_t vr[8];
+    const int rrow0 = lres ? res_row(p, m0) : 0;
+    const __amdgpu_buffer_rsrc_t r_rsrc =
+        make_rsrc(lres ? (const CT*)p.R + (int64_t)rrow0 * p.ldr : (const CT*)p.A, 0x7FFFFFFFu);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        int m = m0 + 8 * (wid + 4 * i) + prow;
+        m = m < p.M ? m : p.M - 1;
+        vr[i] = lres ? (uint32_t)(((res_row(p, m) - rrow0) * p.ldr + lc * 8) * (int)sizeof(CT)) : 0u;
+    }
+    // piece k of part h: wave column k >> 3, the rows of A piece k & 7
+    auto res_piece = [&](char* buf, int k, int h) __attribute__((always_inline)) {
+        const int wcp = k >> 3;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r_rsrc, (lds_ptr_t)(buf + (wcp * 32 + widu + 4 * (k & 7)) * 1024), 16,
+                                                 vr[k & 7], (uint32_t)((n0 + 128 * wcp + 64 * h) * (int)sizeof(CT)),
+                                                 0, 0);
+    };
     // k offset of tile s inside a row: tap * dil rows + channel base (wave-uniform)
     auto a_koff = [&](int s) __attribute__((always_inline)) -> int64_t {
         const int k0 = s * GK;
@@ -161,21 +185,12 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
         return (int64_t)tap * p.dil * p.lda + (k0 - tap * p.Ktap);
     };
     auto dma_piece = [&](char* buf, int i, int s, int64_t aoff) __attribute__((always_inline)) {
-        if constexpr (BUF) {
-            if (i < 8)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(buf + (widu + 4 * i) * 1024), 16, va[i],
-                                                         (uint32_t)aoff * (uint32_t)sizeof(CT), 0, 0);
-            else
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)(buf + GW_OFF + (widu + 4 * (i - 8)) * 1024),
-                                                         16, vw[i - 8], (uint32_t)(s * GK * (int)sizeof(CT)), 0, 0);
-        } else {
-            if (i < 8)
-                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(pa[i] + aoff), (lds_ptr_t)(buf + (widu + 4 * i) * 1024),
-                                                 16, 0, 0);
-            else
-                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(pw[i - 8] + s * GK),
-                                                 (lds_ptr_t)(buf + GW_OFF + (widu + 4 * (i - 8)) * 1024), 16, 0, 0);
-        }
+        if (i < 8)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(buf + (widu + 4 * i) * 1024), 16, va[i],
+                                                     (uint32_t)aoff * (uint32_t)sizeof(CT), 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)(buf + GW_OFF + (widu + 4 * (i - 8)) * 1024),
+                                                     16, vw[i - 8], (uint32_t)(s * GK * (int)sizeof(CT)), 0, 0);
     };
 
     // ---- fragment reads (q64's layout): row (l & 15) of a 16-row block, logical chunk
@@ -190,29 +205,34 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
 
     // 64 MFMAs on set CUR; RD: the 16 reads of set NXT from `rbuf` at k-half offset `fo`;
     // DMA: the 16 pieces of tile `s` into `dbuf`, two per row block
-    auto phase = [&](auto cur_c, auto zero_c, auto rd_c, auto dma_c, const char* rbuf, int fo, char* dbuf,
-                     int s) __attribute__((always_inline)) {
+    auto phase = [&](auto cur_c, auto zero_c, auto rd_c, auto dma_c, const char* rbuf, int fo, char* dbuf, int s,
+                     int resp) __attribute__((always_inline)) {
         constexpr int CUR = decltype(cur_c)::value;
         constexpr int NXT = CUR ^ 1;
         constexpr bool ZERO = decltype(zero_c)::value;
         constexpr bool RD = decltype(rd_c)::value;
         constexpr bool DMA = decltype(dma_c)::value;
         const int64_t aoff = DMA ? a_koff(s) : 0;
+        // each row block: the MFMA on channel block j, with one memory instruction ahead of
+        // the even ones: A read, DMA piece, W read, DMA piece (bursts of 2 reads + 2 pieces
+        // at the row block's start measured 3 % slower at B = 8192, the same at 65,536;
+        // 4 pieces in each of the first 4 row blocks 3-6 % slower).  ABL (measurement
+        // builds): bit 0 no loop DMA, bit 1 no loop fragment reads
+        constexpr bool DO_RD = RD && !(ABL & 2);
+        constexpr bool DO_DMA = DMA && !(ABL & 1);
         static_for<8>([&](auto i_c) __attribute__((always_inline)) {
             constexpr int I = decltype(i_c)::value;
-            if constexpr (RD) {
-                fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
-                fw[NXT][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo);
-            }
-            if constexpr (DMA) {
-                dma_piece(dbuf, 2 * I, s, aoff);
-                dma_piece(dbuf, 2 * I + 1, s, aoff);
-            }
             static_for<8>([&](auto j_c) __attribute__((always_inline)) {
                 constexpr int J = decltype(j_c)::value;
+                if constexpr (DO_RD && J == 0) fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
+                if constexpr (DO_RD && J == 4) fw[NXT][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo);
+                if constexpr (DO_DMA && (J == 2 || J == 6)) dma_piece(dbuf, 2 * I + J / 4, s, aoff);
+                if constexpr (!DMA && (J == 2 || J == 6)) {
+                    if (resp >= 0) res_piece(dbuf, 2 * I + J / 4, resp);
+                }
                 amma<CT, 4 * (8 * I + J), ZERO>(fw[CUR][J], fa[CUR][I]);
+                __builtin_amdgcn_sched_barrier(0);
             });
-            __builtin_amdgcn_sched_barrier(0);
         });
         // the NXT reads (the last issued 8 MFMAs ago) have landed; as a builtin the compiler's
         // own wait bookkeeping sees it, so it adds no lgkmcnt wait behind the next phase's
@@ -221,7 +241,6 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
         if constexpr (RD) __builtin_amdgcn_s_waitcnt(kLgkm0);
     };
 
-    const int nk = p.Kp / GK;  // >= 1
     char* const buf0 = smem;
     char* const buf1 = smem + GBUF;
     {
@@ -245,43 +264,50 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
         fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
     }
 
-    auto mid = [&]() __attribute__((always_inline)) {
-        __builtin_amdgcn_s_waitcnt(kVm0Lgkm0);
+    // last: the 16 residual pieces of part 0 (issued in the phase before) may stay in flight
+    auto mid = [&](bool last) __attribute__((always_inline)) {
+        if (last)
+            __builtin_amdgcn_s_waitcnt(kVm16Lgkm0);
+        else
+            __builtin_amdgcn_s_waitcnt(kVm0Lgkm0);
         pinned_barrier();
     };
     using C0 = std::integral_constant<int, 0>;
     using C1 = std::integral_constant<int, 1>;
     using T_ = std::integral_constant<bool, true>;
     using F_ = std::integral_constant<bool, false>;
-    // K-tile t in buffer `b` (the other one `o`); RD / DMA: tile t + 1 / t + 2 exists
-    auto ktile = [&](auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o) __attribute__((always_inline)) {
-        phase(C0{}, zero_c, T_{}, F_{}, b, fo1, nullptr, 0);
-        mid();
-        phase(C1{}, F_{}, rd_c, dma_c, o, fo0, b, t + 2);
+    // K-tile t in buffer `b` (the other one `o`); RD / DMA: tile t + 1 / t + 2 exists;
+    // resp >= 0: residual part resp into `b` in phase B
+    auto ktile = [&](auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o, int resp) __attribute__((always_inline)) {
+        phase(C0{}, zero_c, T_{}, F_{}, b, fo1, nullptr, 0, -1);
+        mid(resp == 1);
+        phase(C1{}, F_{}, rd_c, dma_c, o, fo0, b, t + 2, resp);
     };
+    const int res0 = lres ? 0 : -1, res1 = lres ? 1 : -1;
     // tile 0 (phase A initialises the accumulators: C = 0), then the steady state (both
-    // follow-up tiles exist: no branch inside a tile), then the last two tiles
+    // follow-up tiles exist: no branch inside a tile), then the last two tiles (with nk >= 3
+    // always the tail's last two calls)
     if (nk > 2)
-        ktile(T_{}, T_{}, T_{}, 0, buf0, buf1);
+        ktile(T_{}, T_{}, T_{}, 0, buf0, buf1, -1);
     else if (nk == 2)
-        ktile(T_{}, T_{}, F_{}, 0, buf0, buf1);
+        ktile(T_{}, T_{}, F_{}, 0, buf0, buf1, -1);
     else
-        ktile(T_{}, F_{}, F_{}, 0, buf0, buf1);
+        ktile(T_{}, F_{}, F_{}, 0, buf0, buf1, -1);
     int t = 1;
     for (; t + 3 < nk; t += 2) {
-        ktile(F_{}, T_{}, T_{}, t, buf1, buf0);
-        ktile(F_{}, T_{}, T_{}, t + 1, buf0, buf1);
+        ktile(F_{}, T_{}, T_{}, t, buf1, buf0, -1);
+        ktile(F_{}, T_{}, T_{}, t + 1, buf0, buf1, -1);
     }
     // 0..3 tiles left, t odd (buffer 1)
     if (t + 2 < nk) {  // three: t, t + 1, t + 2
-        ktile(F_{}, T_{}, T_{}, t, buf1, buf0);
-        ktile(F_{}, T_{}, F_{}, t + 1, buf0, buf1);
-        ktile(F_{}, F_{}, F_{}, t + 2, buf1, buf0);
+        ktile(F_{}, T_{}, T_{}, t, buf1, buf0, -1);
+        ktile(F_{}, T_{}, F_{}, t + 1, buf0, buf1, res0);
+        ktile(F_{}, F_{}, F_{}, t + 2, buf1, buf0, res1);
     } else if (t + 1 < nk) {  // two
-        ktile(F_{}, T_{}, F_{}, t, buf1, buf0);
-        ktile(F_{}, F_{}, F_{}, t + 1, buf0, buf1);
-    } else if (t < nk) {  // one
-        ktile(F_{}, F_{}, F_{}, t, buf1, buf0);
+        ktile(F_{}, T_{}, F_{}, t, buf1, buf0, res0);
+        ktile(F_{}, F_{}, F_{}, t + 1, buf0, buf1, res1);
+    } else if (t < nk) {  // one (nk <= 2: no residual parts)
+        ktile(F_{}, F_{}, F_{}, t, buf1, buf0, -1);
     }
     // the last MFMAs' results -> v_accvgpr_read (inline-asm MFMAs are not tracked by the
     // compiler's hazard recognizer)
@@ -302,12 +328,27 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
                 acc[I][decltype(j_c)::value] = f32x4{aread<R>(), aread<R + 1>(), aread<R + 2>(), aread<R + 3>()};
             });
         });
-        if (p.R)
+        if (lres) {
+            // part H landed: vmcnt(16) leaves in flight only younger pieces / stores (H = 0:
+            // part 1's 16 pieces; H = 1: part 0's epilogue's 16 stores); then every wave's
+            // pieces are visible after the barrier
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            pinned_barrier();
+            const char* rb = smem + ((nk - 2 + H) & 1) * GBUF + wc * 256 * 128 + wr * 128 * 128 + (lane & 15) * 128;
+            const int grp = lane >> 4;
+            const int cq = (grp & 1) * 2 + (grp >> 1);
+            epilogue_tp_rf<CT, 8>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * H, lane, s_scale, s_shift, y_rsrc, m0,
+                                  [&](int i, u32x4(&rr)[2]) __attribute__((always_inline)) {
+                                      rr[0] = *(const u32x4*)(rb + i * 2048 + ((cq ^ fsw) << 4));
+                                      rr[1] = *(const u32x4*)(rb + i * 2048 + (((4 + cq) ^ fsw) << 4));
+                                  });
+        } else if (p.R) {
             epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * H, lane, s_scale, s_shift,
                                             y_rsrc, nullptr, m0);
-        else
+        } else {
             epilogue_tp<CT, 8, false, 0, 0>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * H, lane, s_scale, s_shift,
                                             y_rsrc, nullptr, m0);
+        }
     });
 }
 
@@ -328,21 +369,24 @@ bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
 
 hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream) {
     const dim3 grid(((p.M + GM - 1) / GM) * (p.N / GN));
-    static const bool buf = [] {
-        const char* e = getenv("VP3D_A4_DMA");
-        return !(e && strcmp(e, "global") == 0);
+#ifdef VP3D_ABLATION
+    // measurement builds only (tools/ubench/gemm_check): VP3D_ABL=1 no loop DMA, 2 no loop
+    // fragment reads, 3 neither (wrong results, timing only)
+    static const int abl = [] {
+        const char* e = getenv("VP3D_ABL");
+        return e ? atoi(e) : 0;
     }();
-    if (compute == Act::BF16) {
-        if (buf)
-            hipLaunchKernelGGL((conv_gemm_a4<__bf16, true>), grid, dim3(256), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_a4<__bf16, false>), grid, dim3(256), 0, stream, p);
-    } else {
-        if (buf)
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, true>), grid, dim3(256), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, false>), grid, dim3(256), 0, stream, p);
+    if (compute == Act::BF16 && abl >= 1 && abl <= 3) {
+        if (abl == 1) hipLaunchKernelGGL((conv_gemm_a4<__bf16, 1>), grid, dim3(256), 0, stream, p);
+        else if (abl == 2) hipLaunchKernelGGL((conv_gemm_a4<__bf16, 2>), grid, dim3(256), 0, stream, p);
+        else hipLaunchKernelGGL((conv_gemm_a4<__bf16, 3>), grid, dim3(256), 0, stream, p);
+        return hipGetLastError();
     }
+#endif
+    if (compute == Act::BF16)
+        hipLaunchKernelGGL((conv_gemm_a4<__bf16, 0>), grid, dim3(256), 0, stream, p);
+    else
+        hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0>), grid, dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 

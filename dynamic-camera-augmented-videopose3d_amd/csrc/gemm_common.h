@@ -392,6 +392,61 @@ __device__ __forceinline__ void epilogue_tp(const ConvGemmParams& p, f32x4 (&acc
     }
 }
 
+// epilogue_tp with the residual of row block i fetched by `res_of(i, rr)` from rows already on
+// chip (conv_gemm_a4: landed in LDS by LDS-DMA during the last K-tiles), so no vmcnt waits
+// here; the same arithmetic, so the same bits as epilogue_tp.
+template <typename CT, int MI, typename RF>
+__device__ __forceinline__ void epilogue_tp_rf(const ConvGemmParams& p, f32x4 (&acc)[MI][4], int mw, int nw,
+                                               int lane, const float* s_scale, const float* s_shift,
+                                               __amdgpu_buffer_rsrc_t y_rsrc, int m_base, RF&& res_of) {
+    const int grp = lane >> 4;
+    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+    float sc[4][4], sh[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = nw + 16 * j + 4 * grp;
+        const f32x4 s4 = *(const f32x4*)&s_scale[n];
+        const f32x4 h4 = *(const f32x4*)&s_shift[n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            sc[j][q] = s4[q];
+            sh[j][q] = h4[q];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int m = mw + i * 16 + (lane & 15);
+        u32x4 rr[2];
+        res_of(i, rr);
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+            float v[8];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                float x = __fadd_rn(__fmul_rn(acc[i][2 * jp][d], sc[2 * jp][d]), sh[2 * jp][d]);
+                float y = __fadd_rn(__fmul_rn(acc[i][2 * jp + 1][d], sc[2 * jp + 1][d]), sh[2 * jp + 1][d]);
+                if (p.relu) {
+                    x = x > 0.f ? x : 0.f;
+                    y = y > 0.f ? y : 0.f;
+                }
+                asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+                v[d] = x;
+                v[d + 4] = y;
+            }
+            typedef CT ct8 __attribute__((ext_vector_type(8)));
+            const ct8 r8 = __builtin_bit_cast(ct8, rr[jp]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
+            ct8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (CT)v[e];
+            const uint32_t yo = m < p.M ? (uint32_t)(((size_t)(m - m_base) * p.ldy + nw + 32 * jp + c0) * sizeof(CT))
+                                        : 0xFFFFFFF0u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), y_rsrc, yo, 0, 0);
+        }
+    }
+}
+
 // epilogue_tp for the split-fp16 path (VP3D_DTYPE_F16X3, conv_gemm_q64<_, _, X3>): rows of
 // split activations hold channel n's halves at 64 (n / 32) + n % 32 (hi) and +32 (lo), so
 // a lane's 8 channels nw + 32 jp + c0 + 0..7 are 16 bytes of hi and, 64 bytes on, 16 of lo.

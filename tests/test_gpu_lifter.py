@@ -114,12 +114,12 @@ def test_config4_b65536(dtype):
         assert np.array_equal(y[0], y[reps - 1])
 
 
-@pytest.mark.parametrize("gemm,opt1f", [("big", True), ("8p", True), ("8p", False), ("q64", False),
+@pytest.mark.parametrize("gemm,opt1f", [("big", True), ("8p", True), ("8p", False), ("q64", True), ("q64", False),
                                         ("h16", True), ("h16", False)])
 def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
     """Every 256x256 kernel on the shapes the default dispatch gives another one:
-    VP3D_GEMM=big / 8p put the strided block convs (B = 2050) on the LDS-ring / ping-pong
-    kernel, VP3D_GEMM=8p / q64 the dilated convs of a long sequence on those kernels;
+    VP3D_GEMM=big / 8p / q64 put the strided block convs (B = 2050) on the LDS-ring /
+    ping-pong / quadrant-phase kernel (a4 is the default there), VP3D_GEMM=8p / q64 the dilated convs of a long sequence on those kernels;
     VP3D_GEMM=h16 (measurement override) every large layer on the 128x128 kernel."""
     monkeypatch.setenv("VP3D_GEMM", gemm)
     if opt1f:
@@ -131,12 +131,12 @@ def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 def test_gemm_a4_bit_identical_to_q64(dtype, monkeypatch):
-    """The one-wave-per-SIMD AGPR kernel (conv_gemm_a4.hip) sums every output in q64's K
-    order (two 16x16x32 MFMAs per 64-deep K-tile, K-tiles in order), so every strided
-    k3 conv and 1x1 conv + residual of Optimized1f gives the same bits on either kernel;
-    B = 2050 leaves every layer a ragged last row tile (block 1: 55,350 rows)."""
+    """The one-wave-per-SIMD AGPR kernel (conv_gemm_a4.hip, the default for the strided k3
+    and 1x1 + residual convs with >= 384 tiles) sums every output in q64's K order (two
+    16x16x32 MFMAs per 64-deep K-tile, K-tiles in order), so both give the same bits.
+    B = 4100: blocks 1 and 2 (110,700 / 36,900 rows) run on it with a ragged last row tile."""
     model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
-    x = synth.normalized_windows(1, "x2050_243", 2050, 243)
+    x = synth.normalized_windows(1, "x4100_243", 4100, 243)
     model.cuda().set_compute_dtype(dtype)
     xd = torch.from_numpy(x).cuda()
     ys = {}
@@ -146,9 +146,11 @@ def test_gemm_a4_bit_identical_to_q64(dtype, monkeypatch):
             ys[gemm] = model(xd).cpu().numpy()
     assert np.isfinite(ys["a4"]).all()
     assert np.array_equal(ys["a4"], ys["q64"]), np.abs(ys["a4"] - ys["q64"]).max()
-    ref = lifter_forward(sd, x, [3, 3, 3, 3, 3], causal=False, strided=True, dense=False).numpy()
-    gt = synth.gt_poses(3, "gt", 2050, 17).reshape(ref.shape)
-    _check(ys["a4"], ref, gt, dtype)
+    # the oracle on the first and last 64 windows
+    sel = np.r_[0:64, 4036:4100]
+    ref = lifter_forward(sd, x[sel], [3, 3, 3, 3, 3], causal=False, strided=True, dense=False).numpy()
+    gt = synth.gt_poses(3, "gt", 128, 17).reshape(ref.shape)
+    _check(ys["a4"][sel], ref, gt, dtype)
 
 
 def test_dilated_long_seq_bf16():
