@@ -107,6 +107,14 @@ __device__ __forceinline__ float aread() {
         A4_C10(14), A4_C10(15), A4_C10(16), A4_C10(17), A4_C10(18), A4_C10(19), A4_C10(20), A4_C10(21),          \
         A4_C10(22), A4_C10(23), A4_C10(24), "a250", "a251", "a252", "a253", "a254", "a255"
 
+#ifdef VP3D_ABLATION
+// measurement builds: ABL bit 2 = per-workgroup stamps into g_a4_trace (10 u64 each:
+// 0-3 wall clock (100 MHz) at start / prologue done / K loop done / stores retired, 4 hardware
+// ids, 5-8 shader-clock cycles at the same points, 9 cycles wave 0 spent in the mid waits +
+// barriers; tools/ubench/gemm_check a4t)
+__device__ unsigned long long* g_a4_trace;
+#endif
+
 template <typename CT, int ABL>
 __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     // the accumulator file is this kernel's own from here on (see the header)
@@ -133,6 +141,20 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     const int tile_m = wg / ntn;
     const int tile_n = wg - tile_m * ntn;
     const int m0 = tile_m * GM, n0 = tile_n * GN;
+#ifdef VP3D_ABLATION
+    unsigned long long* const trc = (ABL & 4) && g_a4_trace ? g_a4_trace + (size_t)blockIdx.x * 10 : nullptr;
+    unsigned long long mid_cyc = 0;
+    auto stamp = [&](int slot) __attribute__((always_inline)) {
+        if (trc && tid == 0) {
+            trc[slot] = __builtin_amdgcn_s_memrealtime();
+            trc[slot + 5] = __builtin_amdgcn_s_memtime();
+        }
+    };
+    stamp(0);
+    if (trc && tid == 0)
+        trc[4] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                 __builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
 
     // ---- DMA pieces: 8 rows x 128 B each, 32 per operand; wave w issues q = w + 4 i.
     // Lane l fills row 8q + (l >> 3), physical chunk (l & 7) = logical chunk lc ^ swz; all
@@ -266,11 +288,17 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
 
     // last: the 16 residual pieces of part 0 (issued in the phase before) may stay in flight
     auto mid = [&](bool last) __attribute__((always_inline)) {
+#ifdef VP3D_ABLATION
+        const unsigned long long c0 = (ABL & 4) ? __builtin_amdgcn_s_memtime() : 0;
+#endif
         if (last)
             __builtin_amdgcn_s_waitcnt(kVm16Lgkm0);
         else
             __builtin_amdgcn_s_waitcnt(kVm0Lgkm0);
         pinned_barrier();
+#ifdef VP3D_ABLATION
+        if (ABL & 4) mid_cyc += __builtin_amdgcn_s_memtime() - c0;
+#endif
     };
     using C0 = std::integral_constant<int, 0>;
     using C1 = std::integral_constant<int, 1>;
@@ -284,6 +312,9 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
         phase(C1{}, F_{}, rd_c, dma_c, o, fo0, b, t + 2, resp);
     };
     const int res0 = lres ? 0 : -1, res1 = lres ? 1 : -1;
+#ifdef VP3D_ABLATION
+    stamp(1);
+#endif
     // tile 0 (phase A initialises the accumulators: C = 0), then the steady state (both
     // follow-up tiles exist: no branch inside a tile), then the last two tiles (with nk >= 3
     // always the tail's last two calls)
@@ -312,44 +343,144 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     // the last MFMAs' results -> v_accvgpr_read (inline-asm MFMAs are not tracked by the
     // compiler's hazard recognizer)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#ifdef VP3D_ABLATION
+    stamp(2);
+    if (trc && tid == 0) trc[9] = mid_cyc;
+#endif
 
     // the output resource starts at the tile's first row (outputs past 2^31 bytes: the
     // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
     const size_t y_rest = (size_t)(p.M - m0) * p.ldy * sizeof(CT);
-    const __amdgpu_buffer_rsrc_t y_rsrc =
-        make_rsrc((const CT*)p.Y + (size_t)m0 * p.ldy, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
-    static_for<2>([&](auto h_c) __attribute__((always_inline)) {
+    // ABL bit 3 (measurement): every store dropped by the range check (no output traffic)
+    const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(
+        (const CT*)p.Y + (size_t)m0 * p.ldy, (ABL & 8) ? 0u : (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+    if constexpr ((ABL & 16) != 0) {  // measurement: no epilogue at all (accumulators kept live)
+#ifdef VP3D_ABLATION
+        static_for<64>([&](auto r_c) __attribute__((always_inline)) {
+            asm volatile("" ::"v"(aread<4 * decltype(r_c)::value>()));
+        });
+        if (ABL & 4) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            pinned_barrier();
+            stamp(3);
+        }
+#endif
+        return;
+    }
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    typedef CT ct2 __attribute__((ext_vector_type(2)));
+    typedef CT ct4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const int grp = lane >> 4;
+    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+    // Packed epilogue (ReLU layers; the same bits as gemm::epilogue_tp): per 16 x 64 block the
+    // 16 accumulators of a lane (channels nw + 16 j + 4 grp + 0..3 of one row) leave the AGPRs
+    // and stay in accumulator layout: BN as v_pk_mul_f32 + v_pk_add_f32 (per element the two
+    // roundings of x * scale + shift), with a residual (in LDS: read in accumulator layout,
+    // 8 bytes per block) ReLU as an integer max on the f32 bits (negative and -0 -> +0, as
+    // x > 0 ? x : 0) then the f32 add, one packed conversion per channel pair, without one
+    // ReLU as an integer max on the packed 16-bit pair (the same bits: a pair's sign bit is
+    // set exactly when ReLU-before-rounding gives +0); then one v_permlane16_swap per dword
+    // pair gives each lane 8 consecutive channels for a 16-byte store (epilogue_tp: every
+    // value in f32 through cmp/cndmask ReLU and an f32 swap -- 2.4x the instructions).
+    auto epi_fast = [&](auto h_c, bool with_res) __attribute__((always_inline)) {
         constexpr int H = decltype(h_c)::value;
-        f32x4 acc[8][4];
+        const int nw = n0 + wc * 128 + 64 * H;
+        f32x2 sc[4][2], sh[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = nw + 16 * j + 4 * grp;
+            const f32x4 s4 = *(const f32x4*)&s_scale[n];
+            const f32x4 h4 = *(const f32x4*)&s_shift[n];
+            sc[j][0] = f32x2{s4[0], s4[1]};
+            sc[j][1] = f32x2{s4[2], s4[3]};
+            sh[j][0] = f32x2{h4[0], h4[1]};
+            sh[j][1] = f32x2{h4[2], h4[3]};
+        }
+        // residual part H: row wr * 128 + 16 i + (lane & 15) of wave column wc, channel
+        // 16 j + 4 grp at chunk 2 j + (grp >> 1) (swizzled), byte (grp & 1) * 8
+        const char* rb = smem + ((nk - 2 + H) & 1) * GBUF + wc * 256 * 128 + wr * 128 * 128 + (lane & 15) * 128 +
+                         (grp & 1) * 8;
         static_for<8>([&](auto i_c) __attribute__((always_inline)) {
             constexpr int I = decltype(i_c)::value;
+            const int m = m0 + wr * 128 + 16 * I + (lane & 15);
+            uint32_t pk[4][2];  // [block j][channel pair]
             static_for<4>([&](auto j_c) __attribute__((always_inline)) {
-                constexpr int R = 4 * (8 * I + 4 * H + decltype(j_c)::value);
-                acc[I][decltype(j_c)::value] = f32x4{aread<R>(), aread<R + 1>(), aread<R + 2>(), aread<R + 3>()};
+                constexpr int J = decltype(j_c)::value;
+                constexpr int R = 4 * (8 * I + 4 * H + J);
+                f32x2 v[2] = {f32x2{aread<R>(), aread<R + 1>()}, f32x2{aread<R + 2>(), aread<R + 3>()}};
+                ct4 r4;
+                if (with_res)
+                    r4 = __builtin_bit_cast(
+                        ct4, *(const u32x2*)(rb + I * 2048 + (((2 * J + (grp >> 1)) ^ fsw) << 4)));
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    f32x2 x = v[q] * sc[J][q];
+                    x = x + sh[J][q];
+                    if (with_res) {
+                        i32x2 xi = __builtin_bit_cast(i32x2, x);
+                        xi = __builtin_elementwise_max(xi, i32x2{0, 0});
+                        x = __builtin_bit_cast(f32x2, xi);
+                        x = x + f32x2{(float)r4[2 * q], (float)r4[2 * q + 1]};
+                    }
+                    s16x2 o = __builtin_bit_cast(s16x2, __builtin_convertvector(x, ct2));
+                    if (!with_res) o = __builtin_elementwise_max(o, s16x2{0, 0});
+                    pk[J][q] = __builtin_bit_cast(uint32_t, o);
+                }
             });
+            // the x dwords (blocks 0, 2) just written by VALU -> 2 wait states before the swap
+            asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\t"
+                         "v_permlane16_swap_b32 %4, %5\n\tv_permlane16_swap_b32 %6, %7"
+                         : "+v"(pk[0][0]), "+v"(pk[1][0]), "+v"(pk[0][1]), "+v"(pk[1][1]), "+v"(pk[2][0]),
+                           "+v"(pk[3][0]), "+v"(pk[2][1]), "+v"(pk[3][1]));
+            const uint32_t yo =
+                m < p.M ? (uint32_t)(((size_t)(m - m0) * p.ldy + nw + c0) * sizeof(CT)) : 0xFFFFFFC0u;
+#pragma unroll
+            for (int jp = 0; jp < 2; ++jp)
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    u32x4{pk[2 * jp][0], pk[2 * jp][1], pk[2 * jp + 1][0], pk[2 * jp + 1][1]}, y_rsrc,
+                    m < p.M ? yo + 64 * jp : 0xFFFFFFC0u, 0, 0);
         });
-        if (lres) {
-            // part H landed: vmcnt(16) leaves in flight only younger pieces / stores (H = 0:
-            // part 1's 16 pieces; H = 1: part 0's epilogue's 16 stores); then every wave's
-            // pieces are visible after the barrier
-            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-            pinned_barrier();
-            const char* rb = smem + ((nk - 2 + H) & 1) * GBUF + wc * 256 * 128 + wr * 128 * 128 + (lane & 15) * 128;
-            const int grp = lane >> 4;
-            const int cq = (grp & 1) * 2 + (grp >> 1);
-            epilogue_tp_rf<CT, 8>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * H, lane, s_scale, s_shift, y_rsrc, m0,
-                                  [&](int i, u32x4(&rr)[2]) __attribute__((always_inline)) {
-                                      rr[0] = *(const u32x4*)(rb + i * 2048 + ((cq ^ fsw) << 4));
-                                      rr[1] = *(const u32x4*)(rb + i * 2048 + (((4 + cq) ^ fsw) << 4));
-                                  });
-        } else if (p.R) {
+    };
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    if (lres) {
+        // part H landed: vmcnt(16) leaves in flight only younger pieces / stores (H = 0:
+        // part 1's 16 pieces; H = 1: part 0's epilogue's 16 stores); then every wave's pieces
+        // are visible after the barrier
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        pinned_barrier();
+        epi_fast(H0{}, true);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        pinned_barrier();
+        epi_fast(H1{}, true);
+    } else if (!p.R) {
+        epi_fast(H0{}, false);
+        epi_fast(H1{}, false);
+    } else {  // residual with nk < 3: global loads row block by row block
+        static_for<2>([&](auto h_c) __attribute__((always_inline)) {
+            constexpr int H = decltype(h_c)::value;
+            f32x4 acc[8][4];
+            static_for<8>([&](auto i_c) __attribute__((always_inline)) {
+                constexpr int I = decltype(i_c)::value;
+                static_for<4>([&](auto j_c) __attribute__((always_inline)) {
+                    constexpr int R = 4 * (8 * I + 4 * H + decltype(j_c)::value);
+                    acc[I][decltype(j_c)::value] = f32x4{aread<R>(), aread<R + 1>(), aread<R + 2>(), aread<R + 3>()};
+                });
+            });
             epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * H, lane, s_scale, s_shift,
                                             y_rsrc, nullptr, m0);
-        } else {
-            epilogue_tp<CT, 8, false, 0, 0>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * H, lane, s_scale, s_shift,
-                                            y_rsrc, nullptr, m0);
-        }
-    });
+        });
+    }
+#ifdef VP3D_ABLATION
+    if (ABL & 4) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        pinned_barrier();
+        stamp(3);
+    }
+#endif
 }
 
 #undef A4_C10
@@ -357,8 +488,15 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
 
 }  // namespace
 
+#ifdef VP3D_ABLATION
+hipError_t conv_gemm_a4_set_trace(unsigned long long* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_a4_trace), &buf, sizeof(buf));
+}
+#endif
+
 bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
     if (compute == Act::F32 || a_type != compute || out_type != compute) return false;
+    if (p.relu != 1) return false;  // the packed epilogue is the BN + ReLU one
     if (p.Ktap % GK != 0 || p.Kp % GK != 0 || p.lda % 8 != 0) return false;
     if (p.N % GN != 0 || p.N > GMAXN || p.ldy % 8 != 0 || (p.R && p.ldr % 8 != 0)) return false;
     if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
@@ -376,10 +514,17 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t
         const char* e = getenv("VP3D_ABL");
         return e ? atoi(e) : 0;
     }();
-    if (compute == Act::BF16 && abl >= 1 && abl <= 3) {
-        if (abl == 1) hipLaunchKernelGGL((conv_gemm_a4<__bf16, 1>), grid, dim3(256), 0, stream, p);
-        else if (abl == 2) hipLaunchKernelGGL((conv_gemm_a4<__bf16, 2>), grid, dim3(256), 0, stream, p);
-        else hipLaunchKernelGGL((conv_gemm_a4<__bf16, 3>), grid, dim3(256), 0, stream, p);
+    if (compute == Act::BF16 && abl >= 1) {
+        switch (abl) {
+            case 1: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 1>), grid, dim3(256), 0, stream, p); break;
+            case 2: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 2>), grid, dim3(256), 0, stream, p); break;
+            case 3: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 3>), grid, dim3(256), 0, stream, p); break;
+            case 4: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 4>), grid, dim3(256), 0, stream, p); break;
+            case 8: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 8>), grid, dim3(256), 0, stream, p); break;
+            case 12: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 12>), grid, dim3(256), 0, stream, p); break;
+            case 16: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 16>), grid, dim3(256), 0, stream, p); break;
+            default: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 20>), grid, dim3(256), 0, stream, p); break;
+        }
         return hipGetLastError();
     }
 #endif

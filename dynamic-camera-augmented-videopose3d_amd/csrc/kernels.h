@@ -64,6 +64,8 @@ bool conv_gemm_q64_x3_eligible(const ConvGemmParams& p, bool out_f32);
 hipError_t launch_conv_gemm_q64_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream);
 // measurement only (VP3D_ABL=7 launches): 10 u64 timestamps/ids per workgroup
 hipError_t conv_gemm_8p_set_trace(unsigned long long* buf);
+// measurement builds of conv_gemm_a4.hip only (-DVP3D_ABLATION; VP3D_ABL=4 launches)
+hipError_t conv_gemm_a4_set_trace(unsigned long long* buf);
 
 // Window source for a forward that gathers its input on the fly (vp3d_forward_windows):
 // the B windows are frames [start_b - lead, start_b - lead + window) of device-resident

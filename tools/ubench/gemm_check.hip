@@ -80,16 +80,26 @@ int main(int argc, char** argv) {
     hipMemset(Y, 0, (size_t)M * N * 2);
     p.A = A; p.W = W; p.scale = sc; p.shift = sh; p.R = use_r ? R : nullptr; p.Y = Y;
 
-    const bool trace = !strcmp(kern, "8pt");
+    const bool trace = !strcmp(kern, "8pt") || !strcmp(kern, "a4t");
+    const bool a4t = !strcmp(kern, "a4t");
     unsigned long long* d_trace = nullptr;
     const int nwg_trace = ((M + 255) / 256) * (N / 256);
     if (trace) {
         // the buffer is in place before the first launch (VP3D_ABL=7 launches write it)
         hipMalloc(&d_trace, (size_t)nwg_trace * 80);
         hipMemset(d_trace, 0, (size_t)nwg_trace * 80);
-        if (conv_gemm_8p_set_trace(d_trace) != hipSuccess) { printf("set_trace failed\n"); return 1; }
-        setenv("VP3D_ABL", "7", 1);
-        kern = "8p";
+        if ((a4t ? conv_gemm_a4_set_trace(d_trace) : conv_gemm_8p_set_trace(d_trace)) != hipSuccess) {
+            printf("set_trace failed\n");
+            return 1;
+        }
+        // a4t: VP3D_ABL 4 (default), 12 (stores dropped) or 20 (no epilogue) from the environment
+        if (a4t) {
+            const char* e = getenv("VP3D_ABL");
+            if (!e || (atoi(e) & 4) == 0) setenv("VP3D_ABL", "4", 1);
+        } else {
+            setenv("VP3D_ABL", "7", 1);
+        }
+        kern = a4t ? "a4" : "8p";
     }
     auto launch = [&]() -> hipError_t {
         if (!strcmp(kern, "big")) return launch_conv_gemm_big(p, Act::BF16, Act::BF16, 0);
@@ -148,6 +158,12 @@ int main(int argc, char** argv) {
             const unsigned long long* r = &t[w * 10];
             pro += r[1] - r[0]; loop += r[2] - r[1]; epi += r[3] - r[2];
             cpro += r[6] - r[5]; cloop += r[7] - r[6]; cepi += r[8] - r[7];
+        }
+        if (a4t) {
+            double mid = 0;
+            for (int w = 0; w < nwg; ++w) mid += t[w * 10 + 9];
+            printf("trace: wave 0 in the mid waits + barriers %.0f cycles per WG (%.1f %% of the K loop)\n",
+                   mid / nwg, 100.0 * mid / cloop);
         }
         printf("trace: kernel span %.1f us; per WG mean: prologue %.2f us, K loop %.2f us, epilogue %.2f us"
                " (cycles %.0f / %.0f / %.0f -> %.2f GHz in loop)\n", (t1 - t0) / 100.0, pro / nwg / 100.0,
