@@ -57,6 +57,7 @@ constexpr int GMAXN = 1024;
 constexpr int kLgkm0 = 0xC07F;     // lgkmcnt(0)
 constexpr int kVm0Lgkm0 = 0x0070;  // vmcnt(0) lgkmcnt(0)
 constexpr int kVm16Lgkm0 = 0x4070; // vmcnt(16) lgkmcnt(0)
+constexpr int kVm32Lgkm0 = 0x8070; // vmcnt(32) lgkmcnt(0)
 
 template <typename F, int... Is>
 __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
@@ -91,6 +92,21 @@ __device__ __forceinline__ void amma(const u32x4& w, const u32x4& a) {
     }
 }
 
+// an empty asm on a wave-uniform value: the compiler can no longer see through it (no
+// hoisting or precomputing of what derives from it)
+__device__ __forceinline__ void launder_s(int& x) { asm volatile("" : "+s"(x)); }
+__device__ __forceinline__ void launder_lane_consts(int& a, int& b, int& c, int& d, int& e, int& f, int& g, int& h,
+                                                    int& i) {
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h), "+v"(i));
+}
+// (inline asm with operand constraints lives in __device__ helpers: in a kernel body the host
+// compilation rejects the AMDGPU constraints silently and emits no launch stub)
+__device__ __forceinline__ void launder_params(ConvGemmParams& p) {
+    asm volatile("" : "+s"(p.M), "+s"(p.Kp), "+s"(p.T_out), "+s"(p.T_in), "+s"(p.stride), "+s"(p.dil), "+s"(p.Ktap),
+                 "+s"(p.lda), "+s"(p.R_T), "+s"(p.R_stride), "+s"(p.R_off), "+s"(p.ldr), "+s"(p.ldy));
+    asm volatile("" : "+s"(p.A), "+s"(p.W), "+s"(p.R), "+s"(p.Y));
+}
+
 template <int R>
 __device__ __forceinline__ float aread() {
     float x;
@@ -116,9 +132,12 @@ __device__ unsigned long long* g_a4_trace;
 #endif
 
 template <typename CT, int ABL>
-__global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
+__global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     // the accumulator file is this kernel's own from here on (see the header)
     asm volatile("" ::: A4_ALL_AGPRS);
+    // a copy whose fields go through an empty asm every tile (below): values derived from them
+    // are then recomputed per tile instead of hoisted out of the tile loop and kept live
+    ConvGemmParams p = p_arg;
 
     __shared__ __attribute__((aligned(16))) char smem[2 * GBUF + 2 * GMAXN * 4];
     float* const s_scale = (float*)(smem + 2 * GBUF);
@@ -137,10 +156,14 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
 
     const int ntn = p.N / GN;
     const int ntm = (p.M + GM - 1) / GM;
-    const int wg = xcd_remap(blockIdx.x, ntm * ntn);
-    const int tile_m = wg / ntn;
-    const int tile_n = wg - tile_m * ntn;
-    const int m0 = tile_m * GM, n0 = tile_n * GN;
+    const int ntiles = ntm * ntn;
+    const int nk = p.Kp / GK;  // >= 1
+    // 1x1 convs (residual): the tile's residual rows land in LDS by LDS-DMA during the last
+    // two K-tiles, into the operand buffers those no longer need -- part h (the channel half
+    // h of both wave columns: 256 rows x 2 x 128 B = 64 KiB) in phase B of tile nk - 2 + h,
+    // in the DMA slots; rows at 128-byte pitch with the operands' chunk swizzle -- so the
+    // epilogue reads them from LDS instead of waiting on global loads row block by row block
+    const bool lres = p.R != nullptr && nk >= 3;
 #ifdef VP3D_ABLATION
     unsigned long long* const trc = (ABL & 4) && g_a4_trace ? g_a4_trace + (size_t)blockIdx.x * 10 : nullptr;
     unsigned long long mid_cyc = 0;
@@ -156,51 +179,53 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
                  __builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
 
-    // ---- DMA pieces: 8 rows x 128 B each, 32 per operand; wave w issues q = w + 4 i.
-    // Lane l fills row 8q + (l >> 3), physical chunk (l & 7) = logical chunk lc ^ swz; all
-    // pieces of a wave share the parity of q (= that of w): one swizzled chunk each ----
-    const int prow = lane >> 3;
-    const int lc = (lane & 7) ^ (((wid & 1) * 4 + (prow >> 1)) & 7);
-    // LDS-DMA as buffer_load ... lds through per-tile resources: 32-bit lane offsets fixed
-    // for the launch, the tile's k offset in soffset, so no per-piece address arithmetic
-    // (global_load_lds from 64-bit lane pointers measured 2 % slower: block-1 k3 shape,
-    // B = 8192, 1.251-1.262 vs 1.231-1.237 ms)
-    uint32_t va[8], vw[8];
-    const int srow0 = src_row(p, m0);  // m0 < M; wave-uniform
-    const __amdgpu_buffer_rsrc_t a_rsrc = make_rsrc((const CT*)p.A + (int64_t)srow0 * p.lda, 0x7FFFFFFFu);
-    const __amdgpu_buffer_rsrc_t w_rsrc = make_rsrc((const CT*)p.W + (int64_t)n0 * p.Kp, 0x7FFFFFFFu);
+    // ---- per-tile operand addressing.  DMA pieces: 8 rows x 128 B each, 32 per operand;
+    // wave w issues q = w + 4 i.  Lane l fills row 8q + (l >> 3), physical chunk (l & 7) =
+    // logical chunk lc ^ swz; all pieces of a wave share the parity of q (= that of w): one
+    // swizzled chunk each.  LDS-DMA as buffer_load ... lds through per-tile resources: 32-bit
+    // lane offsets fixed for the tile, the K-tile's k offset in soffset, so no per-piece address
+    // arithmetic (global_load_lds from 64-bit lane pointers measured 2 % slower: block-1 k3
+    // shape, B = 8192, 1.251-1.262 vs 1.231-1.237 ms) ----
+    int prow = lane >> 3;
+    int lc = (lane & 7) ^ (((wid & 1) * 4 + (prow >> 1)) & 7);
+    int m0 = 0, n0 = 0;
+    uint32_t va[8], vw[8], vr[8];
+    __amdgpu_buffer_rsrc_t a_rsrc, w_rsrc, r_rsrc;
+    auto setup = [&](int tix) __attribute__((always_inline)) {
+        const int wg = xcd_remap(tix, ntiles);
+        const int tile_m = wg / ntn;
+        const int tile_n = wg - tile_m * ntn;
+        m0 = tile_m * GM;
+        n0 = tile_n * GN;
+        const int srow0 = src_row(p, m0);  // m0 < M; wave-uniform
+        a_rsrc = make_rsrc((const CT*)p.A + (int64_t)srow0 * p.lda, 0x7FFFFFFFu);
+        w_rsrc = make_rsrc((const CT*)p.W + (int64_t)n0 * p.Kp, 0x7FFFFFFFu);
+        const int rrow0 = lres ? res_row(p, m0) : 0;
+        r_rsrc = make_rsrc(lres ? (const CT*)p.R + (int64_t)rrow0 * p.ldr : (const CT*)p.A, 0x7FFFFFFFu);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        int m = m0 + 8 * (wid + 4 * i) + prow;
-        m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
-        va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lc * 8) * (int)sizeof(CT));
-        vw[i] = (uint32_t)(((8 * (wid + 4 * i) + prow) * p.Kp + lc * 8) * (int)sizeof(CT));  // W rows padded to 256
-    }
-    // 1x1 convs (residual): the tile's residual rows land in LDS by LDS-DMA during the last
-    // two K-tiles, into the operand buffers those no longer need -- part h (the channel half
-    // h of both wave columns: 256 rows x 2 x 128 B = 64 KiB) in phase B of tile nk - 2 + h,
-    // in the DMA slots; rows at 128-byte pitch with the operands' chunk swizzle -- so the
-    // epilogue reads them from LDS instead of waiting on global loads row block by row block
-    const int nk = p.Kp / GK;  // >= 1
-    const bool lres = p.R != nullptr && nk >= 3;
-    uint32_t vr[8];
-    const int rrow0 = lres ? res_row(p, m0) : 0;
-    const __amdgpu_buffer_rsrc_t r_rsrc =
-        make_rsrc(lres ? (const CT*)p.R + (int64_t)rrow0 * p.ldr : (const CT*)p.A, 0x7FFFFFFFu);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        int m = m0 + 8 * (wid + 4 * i) + prow;
-        m = m < p.M ? m : p.M - 1;
-        vr[i] = lres ? (uint32_t)(((res_row(p, m) - rrow0) * p.ldr + lc * 8) * (int)sizeof(CT)) : 0u;
-    }
-    // piece k of part h: wave column k >> 3, the rows of A piece k & 7
+        for (int i = 0; i < 8; ++i) {
+            int m = m0 + 8 * (wid + 4 * i) + prow;
+            m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
+            va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lc * 8) * (int)sizeof(CT));
+            vw[i] = (uint32_t)(((8 * (wid + 4 * i) + prow) * p.Kp + lc * 8) * (int)sizeof(CT));  // W rows padded
+            vr[i] = lres ? (uint32_t)(((res_row(p, m) - rrow0) * p.ldr + lc * 8) * (int)sizeof(CT)) : 0u;
+        }
+    };
+    // piece k of residual part h: wave column k >> 3, the rows of A piece k & 7
+    // LDS-DMA destination of piece slot `q` (of 64 per 64 KiB region) in `buf`: the wave id goes
+    // through an empty asm at every use, so each destination is one scalar add at its
+    // issue instead of 64 precomputed SGPRs kept live across the tile loop
+    auto lds_dst = [&](char* buf, int q) __attribute__((always_inline)) -> char* {
+        int w = widu;
+        launder_s(w);
+        return buf + (w + q) * 1024;
+    };
     auto res_piece = [&](char* buf, int k, int h) __attribute__((always_inline)) {
         const int wcp = k >> 3;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r_rsrc, (lds_ptr_t)(buf + (wcp * 32 + widu + 4 * (k & 7)) * 1024), 16,
-                                                 vr[k & 7], (uint32_t)((n0 + 128 * wcp + 64 * h) * (int)sizeof(CT)),
-                                                 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r_rsrc, (lds_ptr_t)lds_dst(buf, wcp * 32 + 4 * (k & 7)), 16, vr[k & 7],
+                                                 (uint32_t)((n0 + 128 * wcp + 64 * h) * (int)sizeof(CT)), 0, 0);
     };
-    // k offset of tile s inside a row: tap * dil rows + channel base (wave-uniform)
+    // k offset of K-tile s inside a row: tap * dil rows + channel base (wave-uniform)
     auto a_koff = [&](int s) __attribute__((always_inline)) -> int64_t {
         const int k0 = s * GK;
         const int tap = k0 / p.Ktap;
@@ -208,25 +233,39 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     };
     auto dma_piece = [&](char* buf, int i, int s, int64_t aoff) __attribute__((always_inline)) {
         if (i < 8)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)(buf + (widu + 4 * i) * 1024), 16, va[i],
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)lds_dst(buf, 4 * i), 16, va[i],
                                                      (uint32_t)aoff * (uint32_t)sizeof(CT), 0, 0);
         else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)(buf + GW_OFF + (widu + 4 * (i - 8)) * 1024),
-                                                     16, vw[i - 8], (uint32_t)(s * GK * (int)sizeof(CT)), 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)lds_dst(buf + GW_OFF, 4 * (i - 8)), 16, vw[i - 8],
+                                                     (uint32_t)(s * GK * (int)sizeof(CT)), 0, 0);
+    };
+    char* const buf0 = smem;
+    char* const buf1 = smem + GBUF;
+    // K-tiles 0 and 1 of the current tile into buffers 0 and 1
+    auto stage_01 = [&]() __attribute__((always_inline)) {
+        const int64_t o0 = a_koff(0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dma_piece(buf0, i, 0, o0);
+        if (nk > 1) {
+            const int64_t o1 = a_koff(1);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dma_piece(buf1, i, 1, o1);
+        }
     };
 
     // ---- fragment reads (q64's layout): row (l & 15) of a 16-row block, logical chunk
     // 4 kh + (l >> 4), physical chunk ^ ((l & 15) >> 1) ----
-    const int fsw = (lane & 15) >> 1;
-    const int fo0 = (lane & 15) * 128 + (((lane >> 4) ^ fsw) << 4);
-    const int fo1 = (lane & 15) * 128 + ((((lane >> 4) + 4) ^ fsw) << 4);
-    const int a_base = wr * 128 * 128;
-    const int w_base = GW_OFF + wc * 128 * 128;
+    int fsw = (lane & 15) >> 1;
+    int fo0 = (lane & 15) * 128 + (((lane >> 4) ^ fsw) << 4);
+    int fo1 = (lane & 15) * 128 + ((((lane >> 4) + 4) ^ fsw) << 4);
+    int a_base = wr * 128 * 128;
+    int w_base = GW_OFF + wc * 128 * 128;
 
     u32x4 fa[2][8], fw[2][8];  // [set][block]
 
     // 64 MFMAs on set CUR; RD: the 16 reads of set NXT from `rbuf` at k-half offset `fo`;
-    // DMA: the 16 pieces of tile `s` into `dbuf`, two per row block
+    // DMA: the 16 pieces of K-tile `s` into `dbuf`, two per row block; otherwise resp >= 0:
+    // residual part resp into `dbuf` in the same slots
     auto phase = [&](auto cur_c, auto zero_c, auto rd_c, auto dma_c, const char* rbuf, int fo, char* dbuf, int s,
                      int resp) __attribute__((always_inline)) {
         constexpr int CUR = decltype(cur_c)::value;
@@ -263,36 +302,17 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
         if constexpr (RD) __builtin_amdgcn_s_waitcnt(kLgkm0);
     };
 
-    char* const buf0 = smem;
-    char* const buf1 = smem + GBUF;
-    {
-        const int64_t o0 = a_koff(0);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dma_piece(buf0, i, 0, o0);
-    }
-    if (nk > 1) {
-        const int64_t o1 = a_koff(1);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dma_piece(buf1, i, 1, o1);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (younger: tile 1)
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scale / shift stores
-    pinned_barrier();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        fa[0][i] = *(const u32x4*)(buf0 + a_base + i * 2048 + fo0);
-        fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
-    }
-
-    // last: the 16 residual pieces of part 0 (issued in the phase before) may stay in flight
-    auto mid = [&](bool last) __attribute__((always_inline)) {
+    // the wait before a K-tile's phase B: vm = 0 all operand pieces landed; 16: the 16
+    // residual pieces of part 0 (issued in the phase before) may stay in flight; 32: the
+    // previous tile's 32 epilogue stores (younger than this tile's first two K-tiles) may
+    auto mid = [&](int vm) __attribute__((always_inline)) {
 #ifdef VP3D_ABLATION
         const unsigned long long c0 = (ABL & 4) ? __builtin_amdgcn_s_memtime() : 0;
 #endif
-        if (last)
+        if (vm == 16)
             __builtin_amdgcn_s_waitcnt(kVm16Lgkm0);
+        else if (vm == 32)
+            __builtin_amdgcn_s_waitcnt(kVm32Lgkm0);
         else
             __builtin_amdgcn_s_waitcnt(kVm0Lgkm0);
         pinned_barrier();
@@ -304,90 +324,43 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     using C1 = std::integral_constant<int, 1>;
     using T_ = std::integral_constant<bool, true>;
     using F_ = std::integral_constant<bool, false>;
-    // K-tile t in buffer `b` (the other one `o`); RD / DMA: tile t + 1 / t + 2 exists;
+    // K-tile t in buffer `b` (the other one `o`); RD / DMA: K-tile t + 1 / t + 2 exists;
     // resp >= 0: residual part resp into `b` in phase B
-    auto ktile = [&](auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o, int resp) __attribute__((always_inline)) {
+    auto ktile = [&](auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o, int resp, int vm) __attribute__((always_inline)) {
         phase(C0{}, zero_c, T_{}, F_{}, b, fo1, nullptr, 0, -1);
-        mid(resp == 1);
+        mid(vm);
         phase(C1{}, F_{}, rd_c, dma_c, o, fo0, b, t + 2, resp);
     };
-    const int res0 = lres ? 0 : -1, res1 = lres ? 1 : -1;
-#ifdef VP3D_ABLATION
-    stamp(1);
-#endif
-    // tile 0 (phase A initialises the accumulators: C = 0), then the steady state (both
-    // follow-up tiles exist: no branch inside a tile), then the last two tiles (with nk >= 3
-    // always the tail's last two calls)
-    if (nk > 2)
-        ktile(T_{}, T_{}, T_{}, 0, buf0, buf1, -1);
-    else if (nk == 2)
-        ktile(T_{}, T_{}, F_{}, 0, buf0, buf1, -1);
-    else
-        ktile(T_{}, F_{}, F_{}, 0, buf0, buf1, -1);
-    int t = 1;
-    for (; t + 3 < nk; t += 2) {
-        ktile(F_{}, T_{}, T_{}, t, buf1, buf0, -1);
-        ktile(F_{}, T_{}, T_{}, t + 1, buf0, buf1, -1);
-    }
-    // 0..3 tiles left, t odd (buffer 1)
-    if (t + 2 < nk) {  // three: t, t + 1, t + 2
-        ktile(F_{}, T_{}, T_{}, t, buf1, buf0, -1);
-        ktile(F_{}, T_{}, F_{}, t + 1, buf0, buf1, res0);
-        ktile(F_{}, F_{}, F_{}, t + 2, buf1, buf0, res1);
-    } else if (t + 1 < nk) {  // two
-        ktile(F_{}, T_{}, F_{}, t, buf1, buf0, res0);
-        ktile(F_{}, F_{}, F_{}, t + 1, buf0, buf1, res1);
-    } else if (t < nk) {  // one (nk <= 2: no residual parts)
-        ktile(F_{}, F_{}, F_{}, t, buf1, buf0, -1);
-    }
-    // the last MFMAs' results -> v_accvgpr_read (inline-asm MFMAs are not tracked by the
-    // compiler's hazard recognizer)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#ifdef VP3D_ABLATION
-    stamp(2);
-    if (trc && tid == 0) trc[9] = mid_cyc;
-#endif
 
-    // the output resource starts at the tile's first row (outputs past 2^31 bytes: the
-    // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
-    const size_t y_rest = (size_t)(p.M - m0) * p.ldy * sizeof(CT);
-    // ABL bit 3 (measurement): every store dropped by the range check (no output traffic)
-    const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(
-        (const CT*)p.Y + (size_t)m0 * p.ldy, (ABL & 8) ? 0u : (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
-    if constexpr ((ABL & 16) != 0) {  // measurement: no epilogue at all (accumulators kept live)
-#ifdef VP3D_ABLATION
-        static_for<64>([&](auto r_c) __attribute__((always_inline)) {
-            asm volatile("" ::"v"(aread<4 * decltype(r_c)::value>()));
-        });
-        if (ABL & 4) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            pinned_barrier();
-            stamp(3);
-        }
-#endif
-        return;
-    }
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     typedef int i32x2 __attribute__((ext_vector_type(2)));
     typedef short s16x2 __attribute__((ext_vector_type(2)));
     typedef CT ct2 __attribute__((ext_vector_type(2)));
     typedef CT ct4 __attribute__((ext_vector_type(4)));
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    const int grp = lane >> 4;
-    const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
+    int grp = lane >> 4;
+    int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
     // Packed epilogue (ReLU layers; the same bits as gemm::epilogue_tp): per 16 x 64 block the
     // 16 accumulators of a lane (channels nw + 16 j + 4 grp + 0..3 of one row) leave the AGPRs
     // and stay in accumulator layout: BN as v_pk_mul_f32 + v_pk_add_f32 (per element the two
-    // roundings of x * scale + shift), with a residual (in LDS: read in accumulator layout,
-    // 8 bytes per block) ReLU as an integer max on the f32 bits (negative and -0 -> +0, as
-    // x > 0 ? x : 0) then the f32 add, one packed conversion per channel pair, without one
-    // ReLU as an integer max on the packed 16-bit pair (the same bits: a pair's sign bit is
-    // set exactly when ReLU-before-rounding gives +0); then one v_permlane16_swap per dword
-    // pair gives each lane 8 consecutive channels for a 16-byte store (epilogue_tp: every
-    // value in f32 through cmp/cndmask ReLU and an f32 swap -- 2.4x the instructions).
-    auto epi_fast = [&](auto h_c, bool with_res) __attribute__((always_inline)) {
+    // roundings of x * scale + shift), with a residual (read from LDS into registers in
+    // accumulator layout, 8 bytes per block) ReLU as an integer max on the f32 bits (negative
+    // and -0 -> +0, as x > 0 ? x : 0) then the f32 add, one packed conversion per channel pair,
+    // without one ReLU as an integer max on the packed 16-bit pair (the same bits: a pair's
+    // sign bit is set exactly when ReLU-before-rounding gives +0); then one v_permlane16_swap
+    // per dword pair gives each lane 8 consecutive channels for a 16-byte store
+    // (epilogue_tp: every value in f32 through cmp/cndmask ReLU and an f32 swap -- 2.4x the
+    // instructions).  em0 / en0: the tile's origin (m0 / n0 may already be the next tile's).
+    // a residual part in registers (accumulator layout), so its buffer can take one of the
+    // next tile's first two K-tiles before that half's stores
+    u32x2 resr[8][4];
+    auto res_addr = [&](int h, int i, int j) __attribute__((always_inline)) -> const u32x2* {
+        return (const u32x2*)(smem + ((nk - 2 + h) & 1) * GBUF + wc * 256 * 128 + wr * 128 * 128 + (lane & 15) * 128 +
+                              (grp & 1) * 8 + i * 2048 + (((2 * j + (grp >> 1)) ^ fsw) << 4));
+    };
+    auto epi_fast = [&](auto h_c, bool with_res, int em0, int en0, __amdgpu_buffer_rsrc_t y_rsrc) __attribute__((always_inline)) {
         constexpr int H = decltype(h_c)::value;
-        const int nw = n0 + wc * 128 + 64 * H;
+        const int nw = en0 + wc * 128 + 64 * H;
         f32x2 sc[4][2], sh[4][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -399,22 +372,16 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
             sh[j][0] = f32x2{h4[0], h4[1]};
             sh[j][1] = f32x2{h4[2], h4[3]};
         }
-        // residual part H: row wr * 128 + 16 i + (lane & 15) of wave column wc, channel
-        // 16 j + 4 grp at chunk 2 j + (grp >> 1) (swizzled), byte (grp & 1) * 8
-        const char* rb = smem + ((nk - 2 + H) & 1) * GBUF + wc * 256 * 128 + wr * 128 * 128 + (lane & 15) * 128 +
-                         (grp & 1) * 8;
         static_for<8>([&](auto i_c) __attribute__((always_inline)) {
             constexpr int I = decltype(i_c)::value;
-            const int m = m0 + wr * 128 + 16 * I + (lane & 15);
+            const int m = em0 + wr * 128 + 16 * I + (lane & 15);
             uint32_t pk[4][2];  // [block j][channel pair]
             static_for<4>([&](auto j_c) __attribute__((always_inline)) {
                 constexpr int J = decltype(j_c)::value;
                 constexpr int R = 4 * (8 * I + 4 * H + J);
                 f32x2 v[2] = {f32x2{aread<R>(), aread<R + 1>()}, f32x2{aread<R + 2>(), aread<R + 3>()}};
                 ct4 r4;
-                if (with_res)
-                    r4 = __builtin_bit_cast(
-                        ct4, *(const u32x2*)(rb + I * 2048 + (((2 * J + (grp >> 1)) ^ fsw) << 4)));
+                if (with_res) r4 = __builtin_bit_cast(ct4, resr[I][J]);
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
                     f32x2 x = v[q] * sc[J][q];
@@ -435,8 +402,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
                          "v_permlane16_swap_b32 %4, %5\n\tv_permlane16_swap_b32 %6, %7"
                          : "+v"(pk[0][0]), "+v"(pk[1][0]), "+v"(pk[0][1]), "+v"(pk[1][1]), "+v"(pk[2][0]),
                            "+v"(pk[3][0]), "+v"(pk[2][1]), "+v"(pk[3][1]));
-            const uint32_t yo =
-                m < p.M ? (uint32_t)(((size_t)(m - m0) * p.ldy + nw + c0) * sizeof(CT)) : 0xFFFFFFC0u;
+            const uint32_t yo = (uint32_t)(((size_t)(m - em0) * p.ldy + nw + c0) * sizeof(CT));
 #pragma unroll
             for (int jp = 0; jp < 2; ++jp)
                 __builtin_amdgcn_raw_buffer_store_b128(
@@ -446,33 +412,140 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p) {
     };
     using H0 = std::integral_constant<int, 0>;
     using H1 = std::integral_constant<int, 1>;
-    if (lres) {
-        // part H landed: vmcnt(16) leaves in flight only younger pieces / stores (H = 0:
-        // part 1's 16 pieces; H = 1: part 0's epilogue's 16 stores); then every wave's pieces
-        // are visible after the barrier
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    const int res0 = lres ? 0 : -1, res1 = lres ? 1 : -1;
+
+    // ---- the tiles of this workgroup: blockIdx.x, + gridDim.x, ... (a grid of one
+    // workgroup per CU walks them; with one tile per workgroup the loop runs once).  The
+    // next tile's K-tiles 0 and 1 are staged before this tile's epilogue stores (without a
+    // residual in phase B of the last K-tile; with one once the residual is in registers),
+    // so its first waits leave the stores in flight (vmcnt counts in issue order) ----
+    int tix = blockIdx.x;
+    setup(tix);
+    stage_01();
+    bool first = true;
+    for (;;) {
+        // the per-lane constants go through an empty asm every tile: otherwise the compiler
+        // hoists every address derived from them out of the tile loop and keeps them live
+        // across it (past 256 VGPRs, into the accumulator file)
+        launder_lane_consts(prow, lc, fsw, fo0, fo1, a_base, w_base, grp, c0);
+        launder_params(p);
+        const int next = tix + (int)gridDim.x;
+        const bool has_next = next < ntiles;
+        if (first) {
+            if (nk > 1)
+                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // K-tile 0 landed (younger: K-tile 1)
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scale / shift stores
+        } else {
+            // younger: K-tile 1 (16 pieces) and the previous epilogue's 32 stores (with a
+            // residual: the H0 stores, K-tile 1, the H1 stores)
+            asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+        }
         pinned_barrier();
-        epi_fast(H0{}, true);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        pinned_barrier();
-        epi_fast(H1{}, true);
-    } else if (!p.R) {
-        epi_fast(H0{}, false);
-        epi_fast(H1{}, false);
-    } else {  // residual with nk < 3: global loads row block by row block
-        static_for<2>([&](auto h_c) __attribute__((always_inline)) {
-            constexpr int H = decltype(h_c)::value;
-            f32x4 acc[8][4];
-            static_for<8>([&](auto i_c) __attribute__((always_inline)) {
-                constexpr int I = decltype(i_c)::value;
-                static_for<4>([&](auto j_c) __attribute__((always_inline)) {
-                    constexpr int R = 4 * (8 * I + 4 * H + decltype(j_c)::value);
-                    acc[I][decltype(j_c)::value] = f32x4{aread<R>(), aread<R + 1>(), aread<R + 2>(), aread<R + 3>()};
-                });
-            });
-            epilogue_tp<CT, 8, false, 1, 0>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * H, lane, s_scale, s_shift,
-                                            y_rsrc, nullptr, m0);
-        });
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            fa[0][i] = *(const u32x4*)(buf0 + a_base + i * 2048 + fo0);
+            fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
+        }
+        // K-tile 0 (phase A initialises the accumulators: C = 0), then the steady state (both
+        // follow-up K-tiles exist: no branch inside a K-tile), then the last two K-tiles (with
+        // nk >= 3 always the tail's last two calls)
+        // mid(0) of a later tile: K-tile 1 landed, younger stores may stay in flight (32; with
+        // a residual the H1 stores only, 16)
+        const int vm0 = first ? 0 : lres ? 16 : 32;
+        if (nk > 2)
+            ktile(T_{}, T_{}, T_{}, 0, buf0, buf1, -1, vm0);
+        else if (nk == 2)
+            ktile(T_{}, T_{}, F_{}, 0, buf0, buf1, -1, vm0);
+        else
+            ktile(T_{}, F_{}, F_{}, 0, buf0, buf1, -1, vm0);
+#ifdef VP3D_ABLATION
+        if (first) stamp(1);
+#endif
+        const int em0 = m0, en0 = n0;
+        // the next tile's addressing once this tile's last operand DMA has been issued
+        auto next_setup = [&]() __attribute__((always_inline)) {
+            if (has_next) setup(next);
+        };
+        // without a residual: the next tile's K-tiles 0 and 1 in phase B of the last K-tile
+        // (both buffers free), two pieces per DMA slot
+        auto last_ktile = [&](int t, char* b, char* o) __attribute__((always_inline)) {
+            phase(C0{}, F_{}, T_{}, F_{}, b, fo1, nullptr, 0, -1);
+            mid(lres ? 16 : 0);
+            if (lres || !has_next) {
+                phase(C1{}, F_{}, F_{}, F_{}, o, fo0, b, 0, res1);
+            } else {
+                next_setup();
+                phase(C1{}, F_{}, F_{}, F_{}, o, fo0, b, 0, -1);
+                stage_01();
+            }
+        };
+        int t = 1;
+        for (; t + 3 < nk; t += 2) {
+            ktile(F_{}, T_{}, T_{}, t, buf1, buf0, -1, 0);
+            ktile(F_{}, T_{}, T_{}, t + 1, buf0, buf1, -1, 0);
+        }
+        // 0..3 K-tiles left, t odd (buffer 1)
+        if (t + 2 < nk) {  // three: t, t + 1, t + 2
+            ktile(F_{}, T_{}, T_{}, t, buf1, buf0, -1, 0);
+            ktile(F_{}, T_{}, F_{}, t + 1, buf0, buf1, res0, 0);
+            last_ktile(t + 2, buf1, buf0);
+        } else if (t + 1 < nk) {  // two
+            ktile(F_{}, T_{}, F_{}, t, buf1, buf0, res0, 0);
+            last_ktile(t + 1, buf0, buf1);
+        } else if (t < nk) {  // one (nk <= 2: no residual parts)
+            last_ktile(t, buf1, buf0);
+        }
+        // the last MFMAs' results -> v_accvgpr_read (inline-asm MFMAs are not tracked by the
+        // compiler's hazard recognizer)
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#ifdef VP3D_ABLATION
+        stamp(2);
+        if (trc && tid == 0) trc[9] = mid_cyc;
+#endif
+
+        // the output resource starts at the tile's first row (outputs past 2^31 bytes: the
+        // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
+        const size_t y_rest = (size_t)(p.M - em0) * p.ldy * sizeof(CT);
+        const __amdgpu_buffer_rsrc_t y_rsrc =
+            make_rsrc((const CT*)p.Y + (size_t)em0 * p.ldy, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+        if (lres) {
+            // residual part h into registers once landed (every wave's pieces: after the
+            // barrier), then its buffer takes the next tile's K-tile h (nk even: part h sits in
+            // buffer h) before the half-h stores: issue order part 0, part 1, K-tile 0, H0
+            // stores, K-tile 1, H1 stores -- the next tile's first waits pass the stores
+            auto part = [&](auto h_c) __attribute__((always_inline)) {
+                constexpr int H = decltype(h_c)::value;
+                // younger than part h: part 1 (H = 0), or K-tile 0 and the H0 stores (H = 1)
+                if (H == 0 || !has_next)
+                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                pinned_barrier();
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) resr[i][j] = *res_addr(H, i, j);
+                if (has_next) {
+                    __builtin_amdgcn_s_waitcnt(kLgkm0);
+                    pinned_barrier();
+                    if (H == 0) next_setup();
+                    const int64_t o = a_koff(H);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) dma_piece(H == 0 ? buf0 : buf1, i, H, o);
+                }
+                epi_fast(h_c, true, em0, en0, y_rsrc);
+            };
+            part(H0{});
+            part(H1{});
+        } else {  // no residual (the eligibility check leaves no residual with nk < 3)
+            epi_fast(H0{}, false, em0, en0, y_rsrc);
+            epi_fast(H1{}, false, em0, en0, y_rsrc);
+        }
+        if (!has_next) break;
+        tix = next;
+        first = false;
     }
 #ifdef VP3D_ABLATION
     if (ABL & 4) {
@@ -497,6 +570,7 @@ hipError_t conv_gemm_a4_set_trace(unsigned long long* buf) {
 bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
     if (compute == Act::F32 || a_type != compute || out_type != compute) return false;
     if (p.relu != 1) return false;  // the packed epilogue is the BN + ReLU one
+    if (p.R && p.Kp / GK < 3) return false;  // the residual lands in LDS during the last two K-tiles
     if (p.Ktap % GK != 0 || p.Kp % GK != 0 || p.lda % 8 != 0) return false;
     if (p.N % GN != 0 || p.N > GMAXN || p.ldy % 8 != 0 || (p.R && p.ldr % 8 != 0)) return false;
     if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
@@ -506,10 +580,30 @@ bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
 }
 
 hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream) {
-    const dim3 grid(((p.M + GM - 1) / GM) * (p.N / GN));
+    const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+    // Tile walk (one workgroup per CU; a multiple of 8 keeps each workgroup on one XCD's tile
+    // range under round-robin placement) for the 1x1 + residual convs: the next tile's first
+    // two K-tiles then land under this tile's epilogue and no workgroup launch gap separates
+    // the tiles (B = 65,536, same box: block-1 1x1 3.69-3.70 vs 3.78-3.86 ms, blocks 2-4
+    // -4..-8 %); the k3 convs keep one tile per workgroup (walked: the same or up to 2 %
+    // slower).  With a residual the walk needs nk even (residual part h sits in the buffer
+    // of the next tile's K-tile h).  VP3D_A4_WALK (measurement; read at every launch, so a
+    // test can flip it): 0 never, 2 every layer.
+    const char* we = getenv("VP3D_A4_WALK");
+    const int walk_mode = we ? atoi(we) : 1;
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        return n & ~7;
+    }();
+    const int nk = p.Kp / GK;
+    const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && nk >= 3 && ntiles > ncu &&
+                      (!p.R || nk % 2 == 0);
+    const dim3 grid(walk ? ncu : ntiles);
 #ifdef VP3D_ABLATION
     // measurement builds only (tools/ubench/gemm_check): VP3D_ABL=1 no loop DMA, 2 no loop
-    // fragment reads, 3 neither (wrong results, timing only)
+    // fragment reads, 3 neither (wrong results, timing only), 4 stamps
     static const int abl = [] {
         const char* e = getenv("VP3D_ABL");
         return e ? atoi(e) : 0;
@@ -519,11 +613,7 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t
             case 1: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 1>), grid, dim3(256), 0, stream, p); break;
             case 2: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 2>), grid, dim3(256), 0, stream, p); break;
             case 3: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 3>), grid, dim3(256), 0, stream, p); break;
-            case 4: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 4>), grid, dim3(256), 0, stream, p); break;
-            case 8: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 8>), grid, dim3(256), 0, stream, p); break;
-            case 12: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 12>), grid, dim3(256), 0, stream, p); break;
-            case 16: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 16>), grid, dim3(256), 0, stream, p); break;
-            default: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 20>), grid, dim3(256), 0, stream, p); break;
+            default: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 4>), grid, dim3(256), 0, stream, p); break;
         }
         return hipGetLastError();
     }

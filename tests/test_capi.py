@@ -35,6 +35,16 @@ def test_dynamic_symbol_table():
     assert set(header_symbols()) <= exported
 
 
+def test_no_undefined_library_symbols():
+    """Every symbol of the library's own namespace resolves inside it: a kernel whose host-side
+    compilation fails silently (an AMDGPU inline-asm constraint in a kernel body) leaves its
+    launch stub undefined, and the library then fails to load on the GPU box."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", N.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    own = [ln for ln in out.splitlines() if "vp3d" in ln]
+    assert not own, own
+
+
 def test_abi_and_weight_count():
     lib = N.load()
     assert lib.vp3d_abi_version() == 1
