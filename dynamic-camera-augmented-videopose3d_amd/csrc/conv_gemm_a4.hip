@@ -131,7 +131,7 @@ __device__ __forceinline__ float aread() {
 __device__ unsigned long long* g_a4_trace;
 #endif
 
-template <typename CT, int ABL>
+template <typename CT, int ABL, int X3 = 0>
 __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     // the accumulator file is this kernel's own from here on (see the header)
     asm volatile("" ::: A4_ALL_AGPRS);
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     // h of both wave columns: 256 rows x 2 x 128 B = 64 KiB) in phase B of tile nk - 2 + h,
     // in the DMA slots; rows at 128-byte pitch with the operands' chunk swizzle -- so the
     // epilogue reads them from LDS instead of waiting on global loads row block by row block
-    const bool lres = p.R != nullptr && nk >= 3;
+    const bool lres = X3 == 0 && p.R != nullptr && nk >= 3;
 #ifdef VP3D_ABLATION
     unsigned long long* const trc = (ABL & 4) && g_a4_trace ? g_a4_trace + (size_t)blockIdx.x * 10 : nullptr;
     unsigned long long mid_cyc = 0;
@@ -448,6 +448,111 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             fa[0][i] = *(const u32x4*)(buf0 + a_base + i * 2048 + fo0);
             fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
         }
+        if constexpr (X3 != 0) {
+            // ---- split fp16 (VP3D_DTYPE_F16X3): rows hold every f32 value as f16 halves, each
+            // 32-wide K group [hi(32) | lo(32)], so a 64-deep K-tile carries 32 K values: its
+            // k 0..31 fragments are the hi halves, k 32..63 the lo ones.  Per K-tile and
+            // accumulator, in q64's order (the same bits): W_hi.A_hi, W_hi.A_lo, W_lo.A_hi
+            // (the lo.lo term, 2^-22 relative, dropped).  W_hi / W_lo stay in fw[0] / fw[1];
+            // A_hi of K-tile t sits in fa[t & 1], A_lo in the other set:
+            //   A  (64 MFMAs W_hi.A_hi):  reads W_lo -> fw[1], A_lo -> fa[1-h]      (K-tile t)
+            //   mid: vmcnt(0), lgkmcnt(0), barrier
+            //   B1 (64 MFMAs W_hi.A_lo):  A_hi of t + 1 -> fa[1-h], row block i-1 in row block i
+            //                             (its A_lo used up); 8 DMA pieces of t + 2
+            //   B2 (64 MFMAs W_lo.A_hi):  W_hi of t + 1 -> fw[0] (used up in B1); 8 DMA pieces
+            auto x3_phase = [&](auto h_c, auto kind_c, auto zero_c, auto rd_c, auto dma_c, const char* rbuf, char* dbuf,
+                                int s) __attribute__((always_inline)) {
+                constexpr int H = decltype(h_c)::value;
+                constexpr int KIND = decltype(kind_c)::value;  // 0 = A, 1 = B1, 2 = B2
+                constexpr bool ZERO = decltype(zero_c)::value;
+                constexpr bool DO_RD = decltype(rd_c)::value && !(ABL & 2);
+                constexpr bool DO_DMA = decltype(dma_c)::value && !(ABL & 1);
+                const int64_t aoff = DO_DMA ? a_koff(s) : 0;
+                static_for<8>([&](auto i_c) __attribute__((always_inline)) {
+                    constexpr int I = decltype(i_c)::value;
+                    static_for<8>([&](auto j_c) __attribute__((always_inline)) {
+                        constexpr int J = decltype(j_c)::value;
+                        if constexpr (KIND == 0) {
+                            if constexpr (DO_RD && J == 0)
+                                fa[1 - H][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo1);
+                            if constexpr (DO_RD && J == 4)
+                                fw[1][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo1);
+                            amma<CT, 4 * (8 * I + J), ZERO>(fw[0][J], fa[H][I]);
+                        } else if constexpr (KIND == 1) {
+                            if constexpr (DO_RD && J == 0 && I > 0)
+                                fa[1 - H][I - 1] = *(const u32x4*)(rbuf + a_base + (I - 1) * 2048 + fo0);
+                            if constexpr (DO_DMA && J == 4) dma_piece(dbuf, I, s, aoff);
+                            amma<CT, 4 * (8 * I + J), false>(fw[0][J], fa[1 - H][I]);
+                        } else {
+                            if constexpr (DO_RD && J == 0 && I == 0)
+                                fa[1 - H][7] = *(const u32x4*)(rbuf + a_base + 7 * 2048 + fo0);
+                            if constexpr (DO_RD && J == 4) fw[0][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo0);
+                            if constexpr (DO_DMA && J == 2) dma_piece(dbuf, 8 + I, s, aoff);
+                            amma<CT, 4 * (8 * I + J), false>(fw[1][J], fa[H][I]);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    });
+                });
+                if constexpr (KIND == 2 && DO_RD) __builtin_amdgcn_s_waitcnt(kLgkm0);
+            };
+            using K0 = std::integral_constant<int, 0>;
+            using K1 = std::integral_constant<int, 1>;
+            using K2 = std::integral_constant<int, 2>;
+            // K-tile t in buffer `b` (the next one in `o`), A_hi in fa[H]
+            auto x3_ktile = [&](auto h_c, auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o)
+                                __attribute__((always_inline)) {
+                x3_phase(h_c, K0{}, zero_c, T_{}, F_{}, b, nullptr, 0);
+                mid(0);
+                x3_phase(h_c, K1{}, F_{}, rd_c, dma_c, o, b, t + 2);
+                x3_phase(h_c, K2{}, F_{}, rd_c, dma_c, o, b, t + 2);
+            };
+            if (nk > 2)
+                x3_ktile(C0{}, T_{}, T_{}, T_{}, 0, buf0, buf1);
+            else if (nk == 2)
+                x3_ktile(C0{}, T_{}, T_{}, F_{}, 0, buf0, buf1);
+            else
+                x3_ktile(C0{}, T_{}, F_{}, F_{}, 0, buf0, buf1);
+            int t = 1;
+            for (; t + 3 < nk; t += 2) {
+                x3_ktile(C1{}, F_{}, T_{}, T_{}, t, buf1, buf0);
+                x3_ktile(C0{}, F_{}, T_{}, T_{}, t + 1, buf0, buf1);
+            }
+            if (t + 2 < nk) {
+                x3_ktile(C1{}, F_{}, T_{}, T_{}, t, buf1, buf0);
+                x3_ktile(C0{}, F_{}, T_{}, F_{}, t + 1, buf0, buf1);
+                x3_ktile(C1{}, F_{}, F_{}, F_{}, t + 2, buf1, buf0);
+            } else if (t + 1 < nk) {
+                x3_ktile(C1{}, F_{}, T_{}, F_{}, t, buf1, buf0);
+                x3_ktile(C0{}, F_{}, F_{}, F_{}, t + 1, buf0, buf1);
+            } else if (t < nk) {
+                x3_ktile(C1{}, F_{}, F_{}, F_{}, t, buf1, buf0);
+            }
+            asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            // q64's split epilogue (gemm::epilogue_tp_x3) per 64 channels: residual hi + lo
+            // added in f32, output split into hi / lo halves or f32 rows (X3 = 2)
+            constexpr int OB = X3 == 2 ? 4 : 2;  // output element bytes
+            const size_t y_rest = (size_t)(p.M - m0) * p.ldy * OB;
+            const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(
+                (const char*)p.Y + (size_t)m0 * p.ldy * OB, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+            static_for<2>([&](auto hh_c) __attribute__((always_inline)) {
+                constexpr int HH = decltype(hh_c)::value;
+                f32x4 acc[8][4];
+                static_for<8>([&](auto i_c) __attribute__((always_inline)) {
+                    constexpr int I = decltype(i_c)::value;
+                    static_for<4>([&](auto j_c) __attribute__((always_inline)) {
+                        constexpr int R = 4 * (8 * I + 4 * HH + decltype(j_c)::value);
+                        acc[I][decltype(j_c)::value] = f32x4{aread<R>(), aread<R + 1>(), aread<R + 2>(), aread<R + 3>()};
+                    });
+                });
+                if (p.R)
+                    epilogue_tp_x3<X3 == 2, 1>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * HH, lane, s_scale, s_shift,
+                                               y_rsrc, m0);
+                else
+                    epilogue_tp_x3<X3 == 2, 0>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * HH, lane, s_scale, s_shift,
+                                               y_rsrc, m0);
+            });
+            break;  // one tile per workgroup
+        } else {
         // K-tile 0 (phase A initialises the accumulators: C = 0), then the steady state (both
         // follow-up K-tiles exist: no branch inside a K-tile), then the last two K-tiles (with
         // nk >= 3 always the tail's last two calls)
@@ -546,6 +651,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         if (!has_next) break;
         tix = next;
         first = false;
+        }  // X3 == 0
     }
 #ifdef VP3D_ABLATION
     if (ABL & 4) {
@@ -577,6 +683,26 @@ bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
         (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
         return false;
     return (size_t)p.N * p.Kp < (1u << 31);
+}
+
+bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32) {
+    if (p.Ktap % GK != 0 || p.Kp % GK != 0 || p.lda % 8 != 0) return false;
+    if (p.N % GN != 0 || p.N > GMAXN || p.ldy % (out_f32 ? 4 : 8) != 0 || (p.R && p.ldr % 8 != 0)) return false;
+    if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
+        (reinterpret_cast<uintptr_t>(p.W) & 15) || (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
+        return false;
+    // enough tiles to fill the CUs (as the 16-bit dispatch: >= 384 tiles of 256 x 256)
+    if ((int64_t)((p.M + GM - 1) / GM) * (p.N / GN) < 384) return false;
+    return (size_t)p.N * p.Kp < (1u << 31);
+}
+
+hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream) {
+    const dim3 grid(((p.M + GM - 1) / GM) * (p.N / GN));  // one tile per workgroup
+    if (out_f32)
+        hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 2>), grid, dim3(256), 0, stream, p);
+    else
+        hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 1>), grid, dim3(256), 0, stream, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream) {

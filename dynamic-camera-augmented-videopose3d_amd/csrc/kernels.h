@@ -57,6 +57,10 @@ hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_
 // same contract as q64.
 bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream);
+// Split-fp16 mode of conv_gemm_a4 (the q64 contract above, N % 256 == 0, >= 384 tiles); the same
+// bits as conv_gemm_q64_x3.
+bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32);
+hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream);
 // Split-fp16 mode of conv_gemm_q64 (VP3D_DTYPE_F16X3): A / W / residual rows of f16 halves,
 // each 32-wide K group [hi(32) | lo(32)] (Ktap, Kp, lda, ldr in halves); output split
 // (ldy halves) or, out_f32, f32 rows (ldy floats).  N % 64 == 0, N <= 1024.

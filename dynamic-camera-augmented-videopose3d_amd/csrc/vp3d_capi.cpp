@@ -600,8 +600,14 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
             p.scale = L.scale_x3;
             p.ldy = out_f32 ? L.cout : 2 * L.cout;
             if (L.residual) p.ldr = 2 * L.cout;
-            if (!conv_gemm_q64_x3_eligible(p, out_f32)) return fail(VP3D_ERR_ARG, x3_requirement());
-            e = launch_conv_gemm_q64_x3(p, out_f32, s);
+            // the one-wave-per-SIMD kernel where it fills the chip (VP3D_GEMM=q64 forces q64)
+            const char* ge = getenv("VP3D_GEMM");
+            if (!(ge && strcmp(ge, "q64") == 0) && conv_gemm_a4_x3_eligible(p, out_f32)) {
+                e = launch_conv_gemm_a4_x3(p, out_f32, s);
+            } else {
+                if (!conv_gemm_q64_x3_eligible(p, out_f32)) return fail(VP3D_ERR_ARG, x3_requirement());
+                e = launch_conv_gemm_q64_x3(p, out_f32, s);
+            }
             launched = true;
         }
         // the expand kernel takes the BN-folded weights (Layer::wfbf / wfh)

@@ -129,14 +129,16 @@ def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
     _check(y, ref, gt, "bf16")
 
 
-@pytest.mark.parametrize("dtype,walk", [("bf16", None), ("fp16", None), ("bf16", "0"), ("bf16", "2")])
+@pytest.mark.parametrize("dtype,walk", [("bf16", None), ("fp16", None), ("bf16", "0"), ("bf16", "2"),
+                                        ("f16x3", None)])
 def test_gemm_a4_bit_identical_to_q64(dtype, walk, monkeypatch):
     """The one-wave-per-SIMD AGPR kernel (conv_gemm_a4.hip, the default for the strided k3
     and 1x1 + residual convs with >= 384 tiles) sums every output in q64's K order (two
     16x16x32 MFMAs per 64-deep K-tile, K-tiles in order), so both give the same bits.
     B = 4100: blocks 1 and 2 (110,700 / 36,900 rows) run on it with a ragged last row tile.
     walk: VP3D_A4_WALK -- default the 1x1 + residual layers walk their tiles (one workgroup
-    per CU), "0" every layer one tile per workgroup, "2" every layer walks."""
+    per CU), "0" every layer one tile per workgroup, "2" every layer walks.  f16x3: the split
+    fp16 mode (three f16 MFMAs per product, q64's order) against q64's, then the fp32 gates."""
     if walk is not None:
         monkeypatch.setenv("VP3D_A4_WALK", walk)
     model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)

@@ -110,6 +110,10 @@ int main(int argc, char** argv) {
     };
     hipError_t e = launch();
     if (e != hipSuccess) { printf("launch failed: %s\n", hipGetErrorString(e)); return 1; }
+    // VP3D_NOCHECK=1: no reference comparison (timing / stamps of shapes too large to check)
+    double maxe = 0;
+    long bad = 0;
+    if (!getenv("VP3D_NOCHECK")) {
     hipLaunchKernelGGL(ref_kernel, dim3(M, (N + 255) / 256), dim3(256), 0, 0, A, W, sc, sh,
                        use_r ? R : nullptr, Yr, p);
     hipDeviceSynchronize();
@@ -117,8 +121,6 @@ int main(int argc, char** argv) {
     std::vector<float> hYr((size_t)M * N);
     hipMemcpy(hY.data(), Y, hY.size() * 2, hipMemcpyDeviceToHost);
     hipMemcpy(hYr.data(), Yr, hYr.size() * 4, hipMemcpyDeviceToHost);
-    double maxe = 0;
-    long bad = 0;
     for (long i = 0; i < (long)M * N; ++i) {
         const double d = fabs((double)(float)hY[i] - hYr[i]);
         const double tol = 0.02 + 0.01 * fabs(hYr[i]);
@@ -139,6 +141,7 @@ int main(int argc, char** argv) {
             }
             ++bad;
         }
+    }
     }
     printf("%s M=%d N=%d K=%d dil=%d res=%d: max|d|=%.4g  bad=%ld of %ld\n", kern, M, N, K, dil, use_r, maxe,
            bad, (long)M * N);
