@@ -150,7 +150,9 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
                     'extern "C" const char* vp3d_build_hash(void) { return kTag + 16; }\n')
         _run([HIPCC] + COMMON_FLAGS + ["-c", info_src, "-o", info_obj])
         objs.append(info_obj)
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB_PATH] + objs
+        # -z defs: an unresolved symbol (e.g. a kernel launch stub the host compilation dropped)
+        # fails the link here instead of the library load on the GPU box
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,-z,defs", "-o", LIB_PATH] + objs
         if verbose:
             print("$", " ".join(cmd), flush=True)
         _run(cmd)
