@@ -528,28 +528,110 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 x3_ktile(C1{}, F_{}, F_{}, F_{}, t, buf1, buf0);
             }
             asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-            // q64's split epilogue (gemm::epilogue_tp_x3) per 64 channels: residual hi + lo
-            // added in f32, output split into hi / lo halves or f32 rows (X3 = 2)
+            // split epilogue per 64 channels (the arithmetic of gemm::epilogue_tp_x3, so the same
+            // bits): BN as v_pk_mul_f32 + v_pk_add_f32, ReLU as an integer max on the f32 bits,
+            // v_permlane16_swap to 8 consecutive channels per lane, residual hi + lo added in f32,
+            // output split into hi / lo halves (16 bytes each) or f32 rows (X3 = 2).  The
+            // residual of a whole half (8 row blocks x 2 x hi / lo, 128 VGPRs) is loaded up front
+            // -- epilogue_tp_x3 loads it one row block ahead, a latency per row block
             constexpr int OB = X3 == 2 ? 4 : 2;  // output element bytes
             const size_t y_rest = (size_t)(p.M - m0) * p.ldy * OB;
             const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(
                 (const char*)p.Y + (size_t)m0 * p.ldy * OB, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            typedef int i32x2 __attribute__((ext_vector_type(2)));
+            const bool has_r = p.R != nullptr;
+            const int rrow0 = has_r ? res_row(p, m0) : 0;
+            const __amdgpu_buffer_rsrc_t rx_rsrc =
+                make_rsrc(has_r ? (const f16*)p.R + (int64_t)rrow0 * p.ldr : (const f16*)p.A, 0x7FFFFFFFu);
             static_for<2>([&](auto hh_c) __attribute__((always_inline)) {
                 constexpr int HH = decltype(hh_c)::value;
-                f32x4 acc[8][4];
+                const int nw = n0 + wc * 128 + 64 * HH;
+                u32x4 rres[8][2][2];  // [row block][jp][hi, lo]
+                if (has_r) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        int m = m0 + wr * 128 + 16 * i + (lane & 15);
+                        m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
+                        const int off = ((res_row(p, m) - rrow0) * p.ldr + 2 * nw + c0) * 2;
+#pragma unroll
+                        for (int jp = 0; jp < 2; ++jp) {
+                            rres[i][jp][0] = __builtin_bit_cast(
+                                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_rsrc, off + 128 * jp, 0, 0));
+                            rres[i][jp][1] = __builtin_bit_cast(
+                                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_rsrc, off + 128 * jp + 64, 0, 0));
+                        }
+                    }
+                }
+                f32x2 sc[4][2], sh[4][2];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int n = nw + 16 * j + 4 * grp;
+                    const f32x4 s4 = *(const f32x4*)&s_scale[n];
+                    const f32x4 h4 = *(const f32x4*)&s_shift[n];
+                    sc[j][0] = f32x2{s4[0], s4[1]};
+                    sc[j][1] = f32x2{s4[2], s4[3]};
+                    sh[j][0] = f32x2{h4[0], h4[1]};
+                    sh[j][1] = f32x2{h4[2], h4[3]};
+                }
                 static_for<8>([&](auto i_c) __attribute__((always_inline)) {
                     constexpr int I = decltype(i_c)::value;
+                    const int m = m0 + wr * 128 + 16 * I + (lane & 15);
+                    float v4[4][4];  // [block j][element]: BN + ReLU, accumulator layout
                     static_for<4>([&](auto j_c) __attribute__((always_inline)) {
-                        constexpr int R = 4 * (8 * I + 4 * HH + decltype(j_c)::value);
-                        acc[I][decltype(j_c)::value] = f32x4{aread<R>(), aread<R + 1>(), aread<R + 2>(), aread<R + 3>()};
+                        constexpr int J = decltype(j_c)::value;
+                        constexpr int R = 4 * (8 * I + 4 * HH + J);
+                        f32x2 v[2] = {f32x2{aread<R>(), aread<R + 1>()}, f32x2{aread<R + 2>(), aread<R + 3>()}};
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            f32x2 x = v[q] * sc[J][q];
+                            x = x + sh[J][q];
+                            if (p.relu) {
+                                i32x2 xi = __builtin_bit_cast(i32x2, x);
+                                xi = __builtin_elementwise_max(xi, i32x2{0, 0});
+                                x = __builtin_bit_cast(f32x2, xi);
+                            }
+                            v4[J][2 * q] = x[0];
+                            v4[J][2 * q + 1] = x[1];
+                        }
                     });
+#pragma unroll
+                    for (int jp = 0; jp < 2; ++jp) {
+                        float* x = v4[2 * jp];
+                        float* y = v4[2 * jp + 1];
+                        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\t"
+                                     "v_permlane16_swap_b32 %4, %5\n\tv_permlane16_swap_b32 %6, %7"
+                                     : "+v"(x[0]), "+v"(y[0]), "+v"(x[1]), "+v"(y[1]), "+v"(x[2]), "+v"(y[2]),
+                                       "+v"(x[3]), "+v"(y[3]));
+                        float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+                        if (has_r) {
+                            const f16x8 rh = __builtin_bit_cast(f16x8, rres[I][jp][0]);
+                            const f16x8 rl = __builtin_bit_cast(f16x8, rres[I][jp][1]);
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) v[e] += (float)rh[e] + (float)rl[e];
+                        }
+                        const bool in = m < p.M;
+                        if constexpr (X3 == 2) {
+                            const uint32_t yo =
+                                in ? (uint32_t)(((size_t)(m - m0) * p.ldy + nw + 32 * jp + c0) * 4) : 0xFFFFFFE0u;
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                __builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}), y_rsrc, yo, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                __builtin_bit_cast(u32x4, f32x4{v[4], v[5], v[6], v[7]}), y_rsrc, yo + 16, 0, 0);
+                        } else {
+                            f16x8 oh, ol;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) {
+                                oh[e] = (f16)v[e];
+                                ol[e] = (f16)(v[e] - (float)oh[e]);
+                            }
+                            const uint32_t yo =
+                                in ? (uint32_t)(((size_t)(m - m0) * p.ldy + 2 * nw + 64 * jp + c0) * 2) : 0xFFFFFF00u;
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, oh), y_rsrc, yo, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ol), y_rsrc, yo + 64, 0, 0);
+                        }
+                    }
                 });
-                if (p.R)
-                    epilogue_tp_x3<X3 == 2, 1>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * HH, lane, s_scale, s_shift,
-                                               y_rsrc, m0);
-                else
-                    epilogue_tp_x3<X3 == 2, 0>(p, acc, m0 + wr * 128, n0 + wc * 128 + 64 * HH, lane, s_scale, s_shift,
-                                               y_rsrc, m0);
             });
             break;  // one tile per workgroup
         } else {
