@@ -316,13 +316,12 @@ hipError_t launch_f32(const ConvGemmParams& p, bool vepi, dim3 grid, hipStream_t
 }
 
 // Which 256x256 kernel a large layer runs on:
-//   default: for contiguous-tap layers (the strided k-tap convs and the 1x1 convs) with >= 384
-//   tiles the one-wave-per-SIMD AGPR kernel (conv_gemm_a4.hip; block 1 at B = 65,536, same
-//   box: k3 8.65-8.70 vs 9.33 ms on q64, 1x1 + residual 3.99-4.06 vs 4.20-4.22, bit-identical),
-//   then the 64-deep quadrant-phase kernel (conv_gemm_q64.hip) and the ping-pong kernel
-//   (conv_gemm_8p.hip) where a4 is not eligible; the LDS-ring kernel (conv_gemm_big.hip) for
-//   dilated convs (taps gathered from rows d apart; sequence mode, 65,536 frames: 0.39-0.40 vs
-//   0.42 ms).
+//   default: every tap-aligned layer with >= 384 tiles on the one-wave-per-SIMD AGPR kernel
+//   (conv_gemm_a4.hip; block 1 at B = 65,536, same box: k3 8.61-8.64 vs 9.14-9.19 ms on q64,
+//   1x1 + residual 3.57-3.68 vs 4.23; the dilated k3 convs of sequence mode 0.34 vs 0.39 ms on
+//   the LDS-ring kernel; bit-identical to q64), then the 64-deep quadrant-phase kernel
+//   (conv_gemm_q64.hip) and the ping-pong kernel (conv_gemm_8p.hip) where a4 is not eligible,
+//   the LDS-ring kernel (conv_gemm_big.hip) for the dilated layers a4 does not take.
 //   VP3D_GEMM=a4 / q64 / 8p -> that kernel wherever eligible (q64 / 8p: dilated layers included),
 //   VP3D_GEMM=big -> the LDS-ring kernel everywhere; the override tests run each.
 //   VP3D_GEMM=h16 -> the 128x128 kernel everywhere (measurement).
@@ -450,7 +449,7 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
         return hipGetLastError();
     }
     const int gm = gemm_8p_mode();
-    if ((gm == 5 || gm == 1) && p.dil == 1 && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
+    if ((gm == 5 || gm == 1) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_a4_eligible(p, a_type, out_type, compute))
         return launch_conv_gemm_a4(p, compute, stream);
     if ((gm == 3 || (gm == 1 && p.dil == 1)) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&

@@ -159,6 +159,24 @@ def test_gemm_a4_bit_identical_to_q64(dtype, walk, monkeypatch):
     _check(ys["a4"][sel], ref, gt, dtype)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_dilated_seq_a4_bit_identical_to_q64(dtype, monkeypatch):
+    """VP3D_GEMM=a4 puts the dilated k3 convs of a long sequence (taps d rows apart: the tile's
+    k offset steps d rows at every tap) on conv_gemm_a4; q64 sums in the same order.  40,000
+    frames: every block layer has >= 384 tiles of 256 x 256 (both kernels' threshold)."""
+    model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
+    x = synth.normalized_windows(1, "x1_40000", 1, 40000)
+    model.cuda().set_compute_dtype(dtype)
+    xd = torch.from_numpy(x).cuda()
+    ys = {}
+    for gemm in ("q64", "a4"):
+        monkeypatch.setenv("VP3D_GEMM", gemm)
+        with torch.no_grad():
+            ys[gemm] = model(xd).cpu().numpy()
+    assert np.isfinite(ys["a4"]).all()
+    assert np.array_equal(ys["a4"], ys["q64"]), np.abs(ys["a4"] - ys["q64"]).max()
+
+
 def test_dilated_long_seq_bf16():
     # one long sequence: every block layer has >= 384 output tiles, so the dilated
     # taps (row offsets 0, d, 2d) and the residual slice run on the LDS-ring kernel

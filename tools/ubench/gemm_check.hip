@@ -63,7 +63,13 @@ int main(int argc, char** argv) {
     unsigned s = 12345;
     std::vector<bf16> hA((size_t)T_in * Cin), hW((size_t)N * Kp), hR((size_t)T_in * N);
     std::vector<float> hsc(N), hsh(N);
-    for (auto& v : hA) v = (bf16)frand(s);
+    // VP3D_RELU_A=1: A as a ReLU output (about half zeros, the rest positive), as the lifter's
+    // block inputs are
+    const bool relu_a = getenv("VP3D_RELU_A") != nullptr;
+    for (auto& v : hA) {
+        const float x = frand(s);
+        v = (bf16)(relu_a ? (x > 0.f ? x : 0.f) : x);
+    }
     for (auto& v : hW) v = (bf16)(frand(s) * 0.05f);
     for (auto& v : hR) v = (bf16)frand(s);
     for (int n = 0; n < N; ++n) { hsc[n] = 1.0f + 0.5f * frand(s); hsh[n] = 0.1f * frand(s); }
@@ -206,14 +212,17 @@ int main(int argc, char** argv) {
     }
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
-    for (int i = 0; i < 3; ++i) launch();
+    // VP3D_WARM / VP3D_ITERS: untimed / timed launches (default 3 / 10)
+    const int nwarm = getenv("VP3D_WARM") ? atoi(getenv("VP3D_WARM")) : 3;
+    const int niter = getenv("VP3D_ITERS") ? atoi(getenv("VP3D_ITERS")) : 10;
+    for (int i = 0; i < nwarm; ++i) launch();
     hipEventRecord(a, 0);
-    for (int i = 0; i < 10; ++i) launch();
+    for (int i = 0; i < niter; ++i) launch();
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
     float ms;
     hipEventElapsedTime(&ms, a, b);
-    ms /= 10;
+    ms /= niter;
     printf("%s: %.4f ms  %.1f TFLOP/s\n", kern, ms, 2.0 * M * N * K / (ms * 1e-3) / 1e12);
     return bad ? 1 : 0;
 }
