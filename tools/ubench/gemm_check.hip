@@ -52,11 +52,15 @@ int main(int argc, char** argv) {
     const int dil = argc > 5 ? atoi(argv[5]) : 1;
     const int taps = argc > 6 ? atoi(argv[6]) : 3;
     const int use_r = argc > 7 ? atoi(argv[7]) : 0;
-    // one sequence of T_in rows, output T_out = M rows (dilated conv, stride 1)
-    const int T_out = M, T_in = M + (taps - 1) * dil;
+    // one sequence of T_in rows, output T_out = M rows (dilated conv, stride 1: output row m
+    // reads input rows m + tap * dil, so neighbouring rows share input rows).  VP3D_STRIDE=3
+    // with taps 3, dil 1: the Optimized1f strided k3 conv (input rows 3m .. 3m + 2, no sharing:
+    // three times the A traffic of stride 1)
+    const int stride = getenv("VP3D_STRIDE") ? atoi(getenv("VP3D_STRIDE")) : 1;
+    const int T_out = M, T_in = (M - 1) * stride + 1 + (taps - 1) * dil;
     const int K = taps * Cin, Kp = K;
     ConvGemmParams p{};
-    p.M = M; p.N = N; p.K = K; p.Kp = Kp; p.T_out = T_out; p.T_in = T_in; p.stride = 1; p.dil = dil;
+    p.M = M; p.N = N; p.K = K; p.Kp = Kp; p.T_out = T_out; p.T_in = T_in; p.stride = stride; p.dil = dil;
     p.Ktap = Cin; p.lda = Cin; p.relu = 1; p.ldy = N;
     p.R_T = T_in; p.R_stride = 1; p.R_off = (taps - 1) * dil / 2; p.ldr = N;
 
