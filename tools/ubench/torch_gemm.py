@@ -1,7 +1,9 @@
 """Calibration (tool, not product): hipBLASLt bf16 GEMM rate (torch.matmul) on the
 lifter's layer shapes at B = 8192 windows (TORCH_GEMM_B=65536 for the config-4 batch), for
 comparison with the conv-GEMM kernels.  Under rocprofv3 --kernel-trace the kernel names show
-hipBLASLt's tile configuration."""
+hipBLASLt's tile configuration.  TORCH_GEMM_RELU=1: A = relu(randn), the post-ReLU operand the
+block convs see (and gemm_check's VP3D_RELU_A=1): half its products are zero, which changes
+the chip's power draw and so its clock."""
 import os
 
 import torch
@@ -17,6 +19,8 @@ shapes = {  # name: (M, N, K)
 }
 for name, (M, N, K) in shapes.items():
     a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    if os.environ.get("TORCH_GEMM_RELU") == "1":
+        a = torch.relu(a)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
     for _ in range(3):
         torch.matmul(a, w.t())
