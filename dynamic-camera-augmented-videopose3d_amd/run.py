@@ -2,11 +2,14 @@
 """Training and evaluation driver of the temporal-lifter path (drop-in for the FCN
 branch of the reference's run.py: :290-309 model build, :400-417 device and
 checkpoint, :424-590 the training loop, :653-673 its entry, :862-995 per-action
-evaluation).
+evaluation), and the --evaluate path of the fork's trajectory lifters
+(--use-model Transformer | LSTM-Coupled: :311-363 model build, :712-713 the
+sliding_window dispatch).
 
     python run.py -e 60 -c checkpoint --subjects-train S1,S2 --subjects-test S3   # train
     python run.py --evaluate synthetic --fcn-architecture 3,3,3 --subjects-test '*'
     python run.py --evaluate epoch_60.bin -c checkpoint --causal --compute-dtype bf16
+    python run.py --use-model Transformer --evaluate epoch_80.bin -c checkpoint -d CMU
 
 Data: `-d h36m | CMU | CMU_3DPW` reads the reference's .npz layout from --data-dir
 (data_3d_<d>.npz, data_2d_<d>_<keypoints>.npz; the reference hard-codes its paths,
@@ -152,11 +155,47 @@ def _views(data, seqs):
     return cams, p3d, p2d
 
 
+SEQ_MODELS = ("Transformer", "LSTM-Coupled", "LSTM-Uncoupled")
+SEQ_RECEPTIVE_FIELD = 243  # run.py:312 / :334 / :364
+
+
+def build_seq_model(args, J, J_out, announce=True):
+    """--use-model Transformer | LSTM-Coupled | LSTM-Uncoupled (reference run.py:311-393):
+    the fork's trajectory lifters at the parsed hyper-parameters (2D keypoints in, the
+    per-frame camera matrices taken separately by sliding_window).  Weights: the
+    checkpoint's 'model_pos' (run.py:403-409, through the weights-only loader), or with
+    --evaluate synthetic torch's default init under manual_seed(--seed)."""
+    from common.models.CamLSTM import CoupledLSTM, UncoupledLSTM
+    from common.models.CamTransformer import CoupledTransformer
+    if args.model_name == "Transformer":
+        model = CoupledTransformer(J, 2, J_out, 3, d_model=args.d_model, num_layers=args.num_layers,
+                                   n_heads=args.n_heads, dim_feedforward=args.dim_feedforward,
+                                   head_layers=[int(x) for x in args.transformer_head_architecture.split(",")],
+                                   dropout=args.transformer_dropout)
+    else:
+        cls = CoupledLSTM if args.model_name == "LSTM-Coupled" else UncoupledLSTM
+        model = cls(J, 2, J_out, 3, hidden_size=args.lstm_hidden_features, num_cells=args.lstm_cells,
+                    head_layers=[int(x) for x in args.lstm_head_architecture.split(",")],
+                    dropout=args.lstm_dropout)
+    if announce:
+        print('INFO: Trainable parameter count:', sum(p.numel() for p in model.parameters()))
+    if args.evaluate and args.evaluate != "synthetic":
+        path = os.path.join(args.checkpoint, args.evaluate)
+        print('Loading checkpoint', path)
+        ckpt = load_checkpoint(path, trust=args.trust_checkpoint)
+        if "epoch" in ckpt:
+            print('This model was trained for {} epochs'.format(ckpt["epoch"]))
+        model.load_state_dict(ckpt["model_pos"])
+    return model
+
+
 def build_model(args, J, announce=True, J_out=None):
     from common.models.TemporalModel import TemporalModel
     from vp3d_amd import synth
-    fw = [int(x) for x in args.fcn_architecture.split(",")]
     J_out = J if J_out is None else J_out
+    if args.model_name in SEQ_MODELS:
+        return build_seq_model(args, J, J_out, announce)
+    fw = [int(x) for x in args.fcn_architecture.split(",")]
     jin = J + 6 if args.trajectory else J
     model = TemporalModel(jin, 2, J_out, filter_widths=fw, causal=args.causal, dropout=args.fcn_dropout,
                           channels=args.channels, dense=args.dense)
@@ -305,25 +344,40 @@ def main(argv=None):
     from vp3d_amd.evaluate import DeviceMetrics
 
     args = parse_args(argv)
-    if args.model_name != "FCN":
-        raise SystemExit(f"--use-model {args.model_name}: only the FCN lifter runs on this path")
+    seq_model = args.model_name in SEQ_MODELS
+    if args.model_name != "FCN" and not seq_model:
+        if args.model_name == "StackedPoselifter":
+            raise SystemExit("--use-model StackedPoselifter is outside the MI355X path (SURVEY.md §2)")
+        raise KeyError('Invalid model name')  # run.py:392-393
     if not torch.cuda.is_available():
         raise SystemExit("run.py evaluates on the MI355X (no CPU fallback)")
+    if seq_model and not args.evaluate:
+        raise SystemExit(f"--use-model {args.model_name}: training the trajectory lifters is outside the "
+                         "MI355X path (SURVEY.md §8(f)); --evaluate runs them")
+    if seq_model and (args.trajectory or args.compute_dtype != "fp32"):
+        raise SystemExit(f"--use-model {args.model_name} takes the camera matrices itself and runs in fp32 "
+                         "(no --trajectory, --compute-dtype fp32)")
     if not args.evaluate:
         return train_main(args, load_data(args, stride=1))
     if args.subset < 1:
-        raise SystemExit("--subset applies to training (run.py:656); evaluation reads whole sequences")
+        # the reference's evaluation reads whole sequences; --subset only reaches fetch()
+        # for the training views (run.py:217, :232, :656)
+        print("INFO: --subset applies to training views only; evaluating whole sequences")
     data = load_data(args)
     subjects = list(data.keys()) if args.subjects_test in (None, "*") else args.subjects_test.split(",")
     j2, j3 = joint_counts(data)
     model = build_model(args, j2, J_out=j3).cuda().eval()
-    model.set_compute_dtype(args.compute_dtype)
-    pad = (model.receptive_field() - 1) // 2
+    if seq_model:
+        receptive_field = SEQ_RECEPTIVE_FIELD
+    else:
+        model.set_compute_dtype(args.compute_dtype)
+        receptive_field = model.receptive_field()
+    pad = (receptive_field - 1) // 2
     causal_shift = pad if args.causal else 0
 
     def make_generator(cams, p3d, p2d):
         return UnchunkedGenerator(cams, p3d, p2d, pad=pad, causal_shift=causal_shift,
-                                  trajectory=args.trajectory).next_epoch()
+                                  trajectory=args.trajectory)
 
     action_filter = None if args.actions == "*" else args.actions.split(",")
     print('Evaluating...')

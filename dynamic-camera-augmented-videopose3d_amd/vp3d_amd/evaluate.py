@@ -1,8 +1,8 @@
 """Evaluation harness of the FCN path (the part of reference run.py the hot path serves).
 
 Restates run.py:677-774 (`evaluate`) and :906-983 (`run_evaluation`) for the
-temporal lifter: per action, an UnchunkedGenerator over that action's sequences,
-one model call per sequence (run.py:711), Protocol #1 MPJPE accumulated with the
+temporal lifter and the trajectory lifters: per action, an UnchunkedGenerator over
+that action's sequences, one model call per sequence (run.py:710-713), Protocol #1 MPJPE accumulated with the
 reference's N-weighting (run.py:734-738, x1000 -> mm at :762), plus the
 post-path protocols (P-MPJPE :744-747, N-MPJPE :732, MPJVE :750) and the PMCC of
 per-sequence error vs camera motion (:946-983).
@@ -46,17 +46,37 @@ class DeviceMetrics:
         return np.float32(acc[3] / acc[5])
 
 
+def _is_seq_lifter(model) -> bool:
+    try:
+        from common.models.CamLSTM import CamLSTMBase
+        from common.models.CamTransformer import CamTransformerBase
+    except ImportError:  # pragma: no cover - the drop-in package is always importable here
+        return False
+    return isinstance(model, (CamLSTMBase, CamTransformerBase))
+
+
 def evaluate(generator, model: Callable, metrics, action: str | None = None, verbose: bool = True):
-    """One pass over `generator` (yielding (cams, batch_3d, batch_2d, info) with a
-    leading batch axis of 1).  Returns (e1, e2, e3, ev) in mm and per-sequence e1."""
+    """One pass over `generator` -- an UnchunkedGenerator, or any iterable of
+    (cams, batch_3d, batch_2d, info) with a leading batch axis of 1.  The model call
+    follows run.py:710-713: a temporal lifter sees the padded 2D sequence, a trajectory
+    lifter (CamLSTMBase / CamTransformerBase) runs sliding_window(inputs_2d, inputs_cam,
+    generator.seq_length).  Returns (e1, e2, e3, ev) in mm and per-sequence e1."""
     e1 = e2 = e3 = ev = 0.0
     N = 0
     per_seq: List[float] = []
     infos: List[dict] = []
     motion: List[float] = []
+    seq_lifter = _is_seq_lifter(model)
+    seq_length = getattr(generator, "seq_length", None)
+    if seq_lifter and seq_length is None:
+        raise ValueError("a trajectory lifter needs the generator's seq_length (run.py:713)")
+    batches = generator.next_epoch() if hasattr(generator, "next_epoch") else generator
     with torch.no_grad():
-        for cams, batch_3d, batch_2d, info in generator:
-            pred = model(batch_2d)
+        for cams, batch_3d, batch_2d, info in batches:
+            if seq_lifter:
+                pred = model.sliding_window(batch_2d, cams, seq_length)
+            else:
+                pred = model(batch_2d)
             n = batch_3d.shape[0] * batch_3d.shape[1]
             err = metrics.mpjpe(pred, batch_3d)
             e1 += n * err

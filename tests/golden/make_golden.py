@@ -298,12 +298,10 @@ def train_goldens():
     train_case("train_dense_c32", False, F3, 2, 40, channels=32, dense=True)
 
 
-def seq_lifter_case(name, kind, B=6, L=260, seed=0):
-    """Eval-mode CoupledTransformer / CoupledLSTM (CamTransformer.py:95-205,
-    CamLSTM.py:47-129) at the run.py defaults (arguments.py:41-54): forward on B
-    windows of 243 frames and sliding_window over one padded sequence of L frames
-    (run.py:713).  Weights: torch's default init under manual_seed, BN statistics
-    randomised; stored in the fixture."""
+def _ref_seq_model(name, kind, seed):
+    """The reference's CoupledTransformer / CoupledLSTM at the run.py defaults
+    (arguments.py:41-54, run.py:311-363), torch's default init under manual_seed, the
+    LSTM head's BN statistics randomised (eval mode)."""
     from common.models import CamLSTM as ref_lstm
     from common.models import CamTransformer as ref_tfm
     torch.manual_seed(seed)
@@ -319,7 +317,16 @@ def seq_lifter_case(name, kind, B=6, L=260, seed=0):
             bn.running_var.copy_(torch.from_numpy(synth.uniform(seed + i, name + "/var", (n,), 0.5, 2.0).astype(np.float32)))
             bn.weight.data.copy_(torch.from_numpy(synth.uniform(seed + i, name + "/g", (n,), 0.5, 1.5).astype(np.float32)))
             bn.bias.data.copy_(torch.from_numpy(synth.uniform(seed + i, name + "/b", (n,), -0.1, 0.1).astype(np.float32)))
-    m.eval()
+    return m.eval()
+
+
+def seq_lifter_case(name, kind, B=6, L=260, seed=0):
+    """Eval-mode CoupledTransformer / CoupledLSTM (CamTransformer.py:95-205,
+    CamLSTM.py:47-129) at the run.py defaults (arguments.py:41-54): forward on B
+    windows of 243 frames and sliding_window over one padded sequence of L frames
+    (run.py:713).  Weights: torch's default init under manual_seed, BN statistics
+    randomised; stored in the fixture."""
+    m = _ref_seq_model(name, kind, seed)
     x2 = synth.normalized_windows(seed + 1, name, B, 243)
     xc = (synth.normal(seed + 2, name + "/cam", (B, 243, 3, 4), std=0.5)).astype(np.float32)
     s2 = synth.normalized_windows(seed + 3, name + "/seq", 1, L)
@@ -341,6 +348,67 @@ def seq_lifter_case(name, kind, B=6, L=260, seed=0):
 def seq_lifter_goldens():
     seq_lifter_case("cam_transformer", "transformer")
     seq_lifter_case("cam_lstm", "lstm")
+
+
+def run_eval_seq_golden(kind, seed=0):
+    """The reference's --evaluate loop with --use-model Transformer | LSTM-Coupled
+    (run.py:311-363 construction, :697-771 evaluate with the sliding_window dispatch of
+    :712-713 on the reference UnchunkedGenerator's camera matrices, :906-971
+    run_evaluation) on the seeded synthetic split of run_eval_27 (3 subjects x 3
+    actions, 200+ frames).  Weights stored in the fixture."""
+    name = "run_eval_" + kind
+    data = synth.synthetic_split(3, 3, 200, 17, 0, ref_camera.normalize_screen_coordinates)
+    m = _ref_seq_model(name, kind, seed)
+    pad = (243 - 1) // 2  # run.py:313-314 / :335-336
+    actions = {}
+    for s in data:
+        for a in data[s]:
+            actions.setdefault(a.split(" ")[0], []).append((s, a))
+    out = {}
+    e1_seq, infos, motion = [], [], []
+    for key, seqs in actions.items():
+        cams = [data[s][a]["cameras"] for s, a in seqs]
+        p3d = [data[s][a]["positions_3d"] for s, a in seqs]
+        p2d = [data[s][a]["keypoints"] for s, a in seqs]
+        gen = ref_gen.UnchunkedGenerator(cams, p3d, p2d, pad=pad, causal_shift=0)
+        e1 = e2 = e3 = ev = 0.0
+        N = 0
+        with torch.no_grad():
+            for bc, b3, b2, info in gen.next_epoch():
+                x2 = torch.from_numpy(b2.astype("float32"))
+                x3 = torch.from_numpy(b3.astype("float32"))
+                xc = torch.from_numpy(bc.astype("float32"))
+                pred = m.sliding_window(x2, xc, gen.seq_length)
+                err = ref_loss.mpjpe(pred, x3)
+                n = x3.shape[0] * x3.shape[1]
+                e3 += n * ref_loss.n_mpjpe(pred, x3).item()
+                e1 += n * err.item()
+                e1_seq.append(err.numpy())
+                infos.append(info)
+                pm = np.linalg.norm(np.diff(b3, axis=1), axis=-1)
+                motion.append(np.mean(pm.squeeze(), axis=(0, 1)))
+                N += n
+                inp = x3.numpy().reshape(-1, 17, 3)
+                pr = pred.numpy().reshape(-1, 17, 3)
+                e2 += n * ref_loss.p_mpjpe(pr, inp)
+                ev += n * ref_loss.mean_velocity_error(pr, inp)
+        out[key] = np.array([(e1 / N) * 1000, (e2 / N) * 1000, (e3 / N) * 1000, (ev / N) * 1000])
+    corr = np.corrcoef(np.stack([np.array(e1_seq)] + [
+        np.linalg.norm(np.array([i[k] for i in infos]), axis=1)
+        for k in ("cam_velocity", "cam_acceleration", "cam_angular_velocity", "cam_angular_acceleration")]
+        + [np.array(motion)], axis=1))
+    arrays = {"actions": np.array(list(out.keys())), "errors": np.stack(list(out.values())), "pmcc": corr[0, 1:6]}
+    for k, v in m.state_dict().items():
+        if not k.endswith(".pe"):
+            arrays["w/" + k] = v.numpy()
+    arrays["meta"] = np.array(json.dumps(dict(kind=kind, seed=seed, subjects=3, actions=3, frames=200,
+                                              model={"transformer": "Transformer", "lstm": "LSTM-Coupled"}[kind])))
+    save(name, **arrays)
+
+
+def run_eval_seq_goldens():
+    run_eval_seq_golden("transformer")
+    run_eval_seq_golden("lstm")
 
 
 DATASET_DIR = os.path.join(HERE, "datasets")
@@ -662,7 +730,7 @@ def dataset_humaneva_goldens():
 GROUPS = {"run_eval": run_eval_golden, "dataset": dataset_goldens, "dataset_3dpw": dataset_3dpw_goldens,
           "dataset_humaneva": dataset_humaneva_goldens, "model": model_goldens, "generator": generator_goldens,
           "camera": camera_goldens, "projection": projection_goldens, "loss": loss_goldens,
-          "train": train_goldens, "seq_lifter": seq_lifter_goldens}
+          "train": train_goldens, "seq_lifter": seq_lifter_goldens, "run_eval_seq": run_eval_seq_goldens}
 
 if __name__ == "__main__":
     # python make_golden.py [group ...]  (default: every group); the manifest is merged
