@@ -2,22 +2,29 @@
 """Headline benchmark: 3D poses/s of the 243-frame-RF, 17-joint, 1024-channel
 TemporalModelOptimized1f lifter on MI355X (BASELINE.json configs 2 and 4).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch 65536 | --batch B] [--dtype bf16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch 65536 | --batch B] [--dtype f16x3]
 
 One step = one eval-mode forward of the global batch of 243-frame windows (65,536 by
 default: config 4), sharded over the N ranks by vp3d_amd.shard.shard_range, every
 rank's shard gathered on device from one seeded window set and resident in HBM before
-the timed region (strong scaling; N = 1 is the single-GPU config-2/4 point).
+the timed region (strong scaling; N = 1 is the single-GPU config-2/4 point), in the
+split-fp16 path (f16x3: the north-star MPJPE tolerance at 16-bit MFMA rates).
 `value` = G*K / max-over-ranks(wall time of K steps).  --batch B instead gives every
-rank its own B windows (weak scaling).  At N = 1 the line also carries the fp32
-parity path at the same batch (`fp32`), the config-2 batch sweep {1,024, 8,192,
-65,536} and the CPU baseline.
+rank its own B windows (weak scaling).
 
+At N = 1 the line also carries, each with its own roofline, parity and CPU baseline:
+  bf16, fp32    config 2's dtype and the exact parity path on the same windows
+  batch_sweep_poses_per_s   B = 1,024 / 8,192 / 65,536 in f16x3 and bf16
+  config3       trajectory-conditioned windows (K.E + gather + concat in the step): fp16,
+                f16x3, fp32
+  config5       causal streaming, fp16: the hipGraph-pipelined step and one frame in flight
+                (serve latency p50 / p90 / p99)
 Besides the JSON contract fields the line carries
   roofline      dominant kernel (block-1 k3 conv GEMM) FLOP per launch / its average
-                HIP-event duration on the launch stream during the timed steps
+                HIP-event duration on the launch stream during the timed steps; traffic =
+                the committed PMC summary of the same build (null if the build differs)
   cpu_baseline  the oracle (the reference's torch-CPU op sequence) on this host
-  parity        MPJPE delta vs the oracle on a window subset, fp32 and the timed dtype
+  parity        MPJPE delta vs the oracle on a window subset, every dtype
 """
 from __future__ import annotations
 
@@ -57,11 +64,13 @@ def parse():
                     help="windows per GPU per step instead of --global-batch (weak scaling); the per-step "
                          "unit count of --train / --sequence / --seq-model")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp16", "fp32", "f16x3"],
-                    help="bf16 (configs 2/4), fp16 (--traj, --stream); f16x3 = split fp16 (fp32-level "
-                         "accuracy on the 16-bit MFMAs)")
+                    help="default: f16x3 (configs 2/4: split fp16, fp32-level accuracy on the 16-bit MFMAs), "
+                         "fp16 (--traj, --stream)")
     ap.add_argument("--sweep", type=lambda v: [int(t) for t in v.split(",") if t], default=[1024, 8192, 65536],
                     help="config-2 batch sweep on one GPU (windows per step)")
-    ap.add_argument("--no-extras", action="store_true", help="skip the fp32 leg, the sweep and the CPU baseline")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip every leg (the other dtypes, the sweep, configs 3 and 5) and the CPU baseline")
+    ap.add_argument("--no-legs", action="store_true", help="skip the config-3 and config-5 legs of the default line")
     ap.add_argument("--pregathered", action="store_true",
                     help="configs 2/4: time the forward over a window tensor gathered once before the "
                          "timed region (the reference's form: batch built outside the model) instead of "
@@ -111,7 +120,7 @@ def stream_traffic(mode):
         return json.load(f).get("per_step_in_graph_bytes")
 
 
-def stream_main(args, world, rank, dev):
+def stream_main(args, world, rank, dev, emit=True):
     """Config 5: causal TemporalModel, one frame in / one pose out per step.  16-bit
     weights: a graph of Q steps is ONE persistent launch -- by default the layer-pipelined
     form (each CU runs one layer with its weights in VGPRs, the frames of the graph flow
@@ -267,7 +276,10 @@ def stream_main(args, world, rank, dev):
     }
     if cpu:
         out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
-    print(json.dumps(out), flush=True)
+    st.close()
+    if emit:
+        print(json.dumps(out), flush=True)
+    return out
 
 
 RF_FULL = 243
@@ -662,188 +674,284 @@ def profiled_run(lifter, step, steps, warmup, settle_s, world):
     return dt, per_layer, dom
 
 
-def roofline_of(dom, peak, traffic=None):
+def roofline_of(dom, peak, traffic=None, traffic_note=None):
     avg_ms = max(dom["ms_total"] / max(dom["launches"], 1), 1e-9)
     achieved = dom["flop"] / (avg_ms * 1e-3) / 1e12
-    return {"bound": "mfma", "kernel": f"conv_gemm ({LAYER_NAMES[dom['layer']]})", "achieved": round(achieved, 2),
-            "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-            "avg_launch_ms": round(avg_ms, 4), "launches_timed": dom["launches"], "flop_per_launch": dom["flop"]}
+    r = {"bound": "mfma", "kernel": f"conv_gemm ({LAYER_NAMES[dom['layer']]})", "achieved": round(achieved, 2),
+         "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+         "avg_launch_ms": round(avg_ms, 4), "launches_timed": dom["launches"], "flop_per_launch": dom["flop"]}
+    if traffic_note:
+        r["traffic_source"] = traffic_note
+    return r
 
 
-def windows_main(args, world, rank, dev):
-    """Configs 2-4: TemporalModelOptimized1f over 243-frame windows resident in HBM.
+def committed_traffic(dtype, B, traj=False):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary
+    (tools/traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE passes), only when that summary was
+    taken on the library built from these sources (its build_hash); otherwise None, with the
+    stale figure and its provenance in the returned note."""
+    tfile = os.path.join(REPO, "profiles", f"traffic_{dtype}_b{B}{'_traj' if traj else ''}.json")
+    if not os.path.exists(tfile):
+        return None, None
+    with open(tfile) as f:
+        t = json.load(f)
+    from vp3d_amd import _native
+    cur = _native.load().vp3d_build_hash().decode()
+    same = t.get("build_hash") == cur
+    note = {"file": os.path.relpath(tfile, REPO), "build_hash": t.get("build_hash"), "current_build": cur,
+            "same_build": same, "git_commit": t.get("git_commit")}
+    if not same:
+        note["stale_hbm_bytes_per_launch"] = t.get("hbm_bytes_per_launch")
+    return (t.get("hbm_bytes_per_launch") if same else None), note
 
-    Default: a global batch of --global-batch windows (65,536: config 4) sharded over the
-    ranks with vp3d_amd.shard.shard_range (strong scaling; N = 1 is the config-2/4 single-GPU
-    point).  --batch B: B windows per rank (weak scaling).  --traj: config 3, the per-frame
-    K.E + window gather + camera concat inside the step."""
-    from common.models.TemporalModel import TemporalModelOptimized1f
-    from vp3d_amd import synth
-    from vp3d_amd.shard import window_shard
 
-    traj = args.traj
-    dtype = args.dtype or ("fp16" if traj else "bf16")
-    jin = 23 if traj else JOINTS
-    model = TemporalModelOptimized1f(jin, 2, JOINTS, FW, channels=CHANNELS)
-    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    model.eval().cuda()
-    RF = model.receptive_field()
-    pad = (RF - 1) // 2
-    from vp3d_amd.pipeline import SyntheticWindowPool
-    pool = SyntheticWindowPool(1000, dev, cameras=traj)
-    if args.batch:
-        G = args.batch * world
-        s, e = rank * args.batch, (rank + 1) * args.batch
-        pairs = torch.from_numpy(pool.global_pairs(G)[s:e]).to(dev)
-        scaling = "weak"
-    else:
-        G = args.global_batch
-        pairs, s, e = window_shard(pool, G, rank, world, dev)
-        scaling = "strong"
-    B = e - s
-    lifter = model.native_lifter(dev)
-    lifter.reserve(B, RF, dtype)
-    y = torch.empty((B, 1, JOINTS, 3), device=dev)
-    x = None
-    if not traj and args.pregathered:
-        # the rank's shard of the global window set, gathered once on device and resident
-        x = pool.seqs.gather(pairs, RF, pad, "2d").view(B, RF, jin, 2)
+class WindowsCase:
+    """One TemporalModelOptimized1f workload over 243-frame windows resident in HBM (configs 2-4:
+    17 joints; config 3: 23 "joints" = keypoints + the 12 K.E channels).
 
-    def make_step(dt_, x_, pairs_, y_):
-        if traj:
+    G windows of one seeded global set (vp3d_amd.pipeline.SyntheticWindowPool), this rank's
+    shard gathered on device inside every step (fused into the expand conv on the 16-bit and
+    split-fp16 paths); config 3 also recomputes the per-frame K.E inside the step."""
+
+    def __init__(self, traj, G, rank, world, dev, batch=None, pregathered=False):
+        from common.models.TemporalModel import TemporalModelOptimized1f
+        from vp3d_amd import synth
+        from vp3d_amd.pipeline import SyntheticWindowPool
+        from vp3d_amd.shard import window_shard
+        self.traj, self.dev = traj, dev
+        self.jin = 23 if traj else JOINTS
+        model = TemporalModelOptimized1f(self.jin, 2, JOINTS, FW, channels=CHANNELS)
+        self.sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in self.sd.items()})
+        model.eval().cuda()
+        self.RF = model.receptive_field()
+        self.pad = (self.RF - 1) // 2
+        self.pool = SyntheticWindowPool(1000, dev, cameras=traj)
+        if batch:
+            self.G = batch * world
+            s, e = rank * batch, (rank + 1) * batch
+            self.pairs = torch.from_numpy(self.pool.global_pairs(self.G)[s:e]).to(dev)
+            self.scaling = "weak"
+        else:
+            self.G = G
+            self.pairs, s, e = window_shard(self.pool, G, rank, world, dev)
+            self.scaling = "strong"
+        self.B = e - s
+        self.lifter = model.native_lifter(dev)
+        self.x = None
+        if not traj and pregathered:
+            self.x = self.pool.seqs.gather(self.pairs, self.RF, self.pad, "2d").view(self.B, self.RF, self.jin, 2)
+        self.flop_pose = 358541312 if traj else 352569344
+        self._ref = None
+
+    def make_step(self, dtype, y, pairs=None, x=None):
+        pairs = self.pairs if pairs is None else pairs
+        lifter, seqs, RF, pad = self.lifter, self.pool.seqs, self.RF, self.pad
+        if self.traj:
             def step():
                 # config 3: K.E of every frame, then the window gather + camera concat fused
                 # into the expand conv's operand loads, then the stack
-                pool.seqs.refresh_cameras()
-                lifter.forward_windows(pool.seqs, pairs_, RF, pad, concat_cams=True, dtype=dt_, out=y_)
-        elif x_ is None:
+                seqs.refresh_cameras()
+                lifter.forward_windows(seqs, pairs, RF, pad, concat_cams=True, dtype=dtype, out=y)
+        elif x is None:
             def step():
                 # configs 2/4: the batch of the step (ChunkedGenerator's window gather with
                 # edge clamping, generators.py:102-137) assembled on device from the resident
-                # sequences -- fused into the expand conv's operand loads on the 16-bit path --
-                # then the stack (TemporalModel.py:62-76)
-                lifter.forward_windows(pool.seqs, pairs_, RF, pad, concat_cams=False, dtype=dt_, out=y_)
+                # sequences, then the stack (TemporalModel.py:62-76)
+                lifter.forward_windows(seqs, pairs, RF, pad, concat_cams=False, dtype=dtype, out=y)
         else:
             def step():
-                lifter.forward(x_, dt_, out=y_)
+                lifter.forward(x, dtype, out=y)
         return step
 
-    with torch.no_grad():
-        dt, per_layer, dom = profiled_run(lifter, make_step(dtype, x, pairs, y), args.steps, args.warmup,
-                                          args.settle_seconds, world)
+    def run(self, dtype, steps, warmup, settle_s, world):
+        """Time `steps` steps in `dtype`; returns (seconds, per-layer ms, dominant record, output)."""
+        y = torch.empty((self.B, 1, JOINTS, 3), device=self.dev)
+        self.lifter.reserve(self.B, self.RF, dtype)
+        with torch.no_grad():
+            dt, per_layer, dom = profiled_run(self.lifter, self.make_step(dtype, y, x=self.x), steps, warmup,
+                                              settle_s, world)
+        return dt, per_layer, dom, y
+
+    def parity_ref(self, P):
+        """The oracle on P windows from both ends of the shard (rank 0), once per case."""
+        if self._ref is None:
+            from oracle.temporal_ref import lifter_forward
+            from vp3d_amd import synth
+            P = min(P, self.B)
+            idx = torch.cat([torch.arange(P // 2), torch.arange(self.B - (P - P // 2), self.B)]).to(self.dev)
+            xs = self.pool.seqs.gather(self.pairs[idx].contiguous(), self.RF, self.pad, "2d",
+                                       concat_cams=self.traj).view(P, self.RF, self.jin, 2)
+            ref = lifter_forward(self.sd, xs.cpu(), FW, strided=True).numpy()
+            gt = synth.gt_poses(3, "bench_gt", P, JOINTS).reshape(ref.shape)
+            self._ref = (idx, ref, gt)
+        return self._ref
+
+    def parity(self, y, P):
+        idx, ref, gt = self.parity_ref(P)
+        yf = y[idx].cpu().numpy()
+
+        def mp(a):
+            return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
+        return {"mpjpe_delta_mm": abs(mp(yf) - mp(ref)) * 1e3,
+                "max_coord_delta_mm": float(np.abs(yf - ref).max()) * 1e3,
+                "meets_north_star_1e-4mm": bool(abs(mp(yf) - mp(ref)) * 1e3 <= 1e-4)}
+
+    def parity_info(self, P):
+        idx, ref, gt = self.parity_ref(P)
+        return {"windows": int(idx.numel()), "windows_checked": "first and last half of rank 0's shard "
+                "(the timed kernels' own output)",
+                "mpjpe_ref_mm": round(float(np.mean(np.linalg.norm(ref.astype(np.float64) - gt, axis=-1))) * 1e3, 6),
+                "output_rms_m": round(float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))), 6)}
+
+    def cpu_baseline(self, seconds):
+        from oracle.temporal_ref import lifter_forward
+        xc = self.pool.seqs.gather(self.pairs[:64].contiguous(), self.RF, self.pad, "2d",
+                                   concat_cams=self.traj).view(-1, self.RF, self.jin, 2).cpu()
+        sd = self.sd
+        return cpu_baseline(lambda: lifter_forward(sd, xc, FW, strided=True), int(xc.shape[0]), "poses/s",
+                            f"windows of 243x{self.jin}x2 through oracle/temporal_ref.py (torch-CPU, fp32, batch "
+                            f"{int(xc.shape[0])})", target_s=seconds / 5)
+
+    def leg(self, dtype, steps, warmup, settle_s, P, G=None):
+        """One dtype on this case (rank 0, N = 1): rate, roofline, per-layer times, parity."""
+        dt, per_layer, dom, y = self.run(dtype, steps, warmup, settle_s, 1)
+        traffic, tnote = committed_traffic(dtype, self.B, self.traj)
+        out = {"value": round((G or self.G) * steps / dt, 2), "unit": "poses/s", "steps": steps,
+               "ms_per_step": round(dt / steps * 1e3, 4),
+               "tflops_effective": round((G or self.G) * steps / dt * self.flop_pose / 1e12, 2),
+               "roofline": roofline_of(dom, PEAK_TFLOPS[dtype], traffic, tnote), "per_layer_ms": per_layer,
+               **self.parity(y, P)}
+        if dtype == "f16x3":
+            out["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per algorithmic "
+                                            "multiply-add (hi.hi + hi.lo + lo.hi)")
+        del y
+        return out
+
+    def close(self):
+        self.lifter.close()
+        self.x = None
+
+
+def windows_main(args, world, rank, dev):
+    """Configs 2-4 (default: config 4 at N ranks), or config 3 with --traj.
+
+    Default line: a global batch of --global-batch windows (65,536: config 4) sharded over the
+    ranks with vp3d_amd.shard.shard_range (strong scaling; N = 1 is the config-2/4 single-GPU
+    point), timed in the accurate split-fp16 path (f16x3: the north-star tolerance at MFMA
+    rates).  --batch B: B windows per rank (weak scaling).  At N = 1 the line also carries
+    the bf16 (config 2's dtype) and fp32 legs, the batch sweep, config 3 (fp16 / f16x3 / fp32)
+    and config 5 (causal streaming) as legs, each with its roofline, parity and CPU baseline."""
+    traj = args.traj
+    dtype = args.dtype or ("fp16" if traj else "f16x3")
+    case = WindowsCase(traj, args.global_batch, rank, world, dev, args.batch, args.pregathered)
+    G, B = case.G, case.B
+    dt, per_layer, dom, y = case.run(dtype, args.steps, args.warmup, args.settle_seconds, world)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    value = G * args.steps / dt if scaling == "strong" else world * B * args.steps / dt
+    value = G * args.steps / dt if case.scaling == "strong" else world * B * args.steps / dt
     if rank != 0:
         return
-
-    from oracle.temporal_ref import lifter_forward
-    flop_pose = 358541312 if traj else 352569344
-
-    # ---- parity: the timed kernels' own output on windows from both ends of the shard ----
-    P = min(args.parity_windows, B)
-    idx = torch.cat([torch.arange(P // 2), torch.arange(B - (P - P // 2), B)]).to(dev)
-    xs = pool.seqs.gather(pairs[idx].contiguous(), RF, pad, "2d", concat_cams=traj).view(P, RF, jin, 2)
-    y_fast = y[idx].cpu().numpy()
-    ref = lifter_forward(sd, xs.cpu(), FW, strided=True).numpy()
-    gt = synth.gt_poses(3, "bench_gt", P, JOINTS).reshape(ref.shape)
-
-    def mp(a):
-        return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
-    parity = {"windows": P, "windows_checked": "first and last half of rank 0's shard (timed kernels' output)",
-              "mpjpe_ref_mm": round(mp(ref) * 1e3, 6),
-              "output_rms_m": round(float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))), 6),
-              f"{dtype}_mpjpe_delta_mm": abs(mp(y_fast) - mp(ref)) * 1e3,
-              f"{dtype}_max_coord_delta_mm": float(np.abs(y_fast - ref).max()) * 1e3}
-
-    def committed_traffic(dt):
-        """HBM bytes per launch of the dominant kernel from the committed PMC summary
-        (tools/traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE passes), or None."""
-        tfile = os.path.join(REPO, "profiles", f"traffic_{dt}_b{B}{'_traj' if traj else ''}.json")
-        if os.path.exists(tfile):
-            with open(tfile) as f:
-                return json.load(f).get("hbm_bytes_per_launch")
-        return None
-    traffic = committed_traffic(dtype)
+    P = args.parity_windows
+    parity = dict(case.parity_info(P), **{f"{dtype}_{k}": v for k, v in case.parity(y, P).items()})
+    del y
+    traffic, tnote = committed_traffic(dtype, B, traj)
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": dtype,
+        "scaling": case.scaling, "vs_baseline": None, "dtype": dtype,
+        "dtype_note": ("f16x3 = split fp16: every f32 value carried as f16 hi + lo, three f16 MFMA products per "
+                       "multiply-add accumulated in f32 -- the accuracy of the reference's fp32 (parity below) at "
+                       "16-bit MFMA rates" if dtype == "f16x3" else None),
         "data": "synthetic (seeded random-walk 2D keypoint tracks gathered into windows on device, "
                 "counter-hash weights)",
         "config": {
             "workload": ("config3 trajectory-conditioned (46ch) " if traj else
-                         ("config4 global batch sharded over ranks, " if scaling == "strong" else "config2 ")
+                         ("config4 global batch sharded over ranks, " if case.scaling == "strong" else "config2 ")
                          ) + "TemporalModelOptimized1f 243-frame RF windows, 17 joints, 1024 ch" +
-                        ("; windows pre-gathered before the timed region" if x is not None else
+                        ("; windows pre-gathered before the timed region" if case.x is not None else
                          "; window batch assembled on device from resident sequences inside the step"),
             "global_batch": G, "windows_per_gpu": B,
             "parallelism": f"dp{world} (contiguous shards of one global window set, no collective)"
-            if scaling == "strong" else f"dp{world} (independent windows per rank, no collective)",
-            "flop_per_pose": flop_pose},
-        "tflops_effective": round(value * flop_pose / 1e12, 2),
-        "roofline": roofline_of(dom, PEAK_TFLOPS[dtype], traffic),
+            if case.scaling == "strong" else f"dp{world} (independent windows per rank, no collective)",
+            "flop_per_pose": case.flop_pose},
+        "tflops_effective": round(value * case.flop_pose / 1e12, 2),
+        "roofline": roofline_of(dom, PEAK_TFLOPS[dtype], traffic, tnote),
         "per_layer_ms": per_layer,
         "per_layer_note": "untimed pass with HIP events around every launch",
         "parity": parity,
     }
-
-    if world == 1 and not args.no_extras:
-        with torch.no_grad():
-            # ---- the parity-gate paths: exact fp32 and split fp16 (f16x3), same windows and B
-            # (config 3: the f16x3 leg, its accurate dtype) ----
-            legs = [("f16x3", max(5, args.steps // 2))]
-            if not traj:
-                legs.insert(0, ("fp32", max(3, args.steps // 4)))
-            for dt_acc, ksteps in legs:
-                if dt_acc == dtype:
+    if dtype == "f16x3":
+        out["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per algorithmic "
+                                        "multiply-add (hi.hi + hi.lo + lo.hi)")
+    if world > 1 or args.no_extras:
+        print(json.dumps(out), flush=True)
+        return
+    legs = ["bf16", "fp32"] if not traj else ["f16x3", "fp32"]
+    for dl in legs:
+        if dl == dtype:
+            continue
+        ks = max(3, args.steps // 4) if dl == "fp32" else max(5, args.steps // 2)
+        out[dl] = case.leg(dl, ks, 1, 0.3, P)
+        parity[f"{dl}_mpjpe_delta_mm"] = out[dl]["mpjpe_delta_mm"]
+        parity[f"{dl}_max_coord_delta_mm"] = out[dl]["max_coord_delta_mm"]
+    if not traj:
+        # ---- config-2 batch sweep (1 GPU), the timed dtype and bf16 ----
+        sweep = {}
+        for sdt in dict.fromkeys([dtype, "bf16"]):
+            row = {}
+            for Bs in args.sweep:
+                if Bs == B and sdt == dtype:
+                    row[str(Bs)] = round(value, 2)
                     continue
-                ya = torch.empty_like(y)
-                lifter.reserve(B, RF, dt_acc)
-                dta, pla, doma = profiled_run(lifter, make_step(dt_acc, x, pairs, ya), ksteps, 1, 0.3, 1)
-                yas = ya[idx].cpu().numpy()
-                out[dt_acc] = {"value": round(G * ksteps / dta, 2), "unit": "poses/s", "steps": ksteps,
-                               "ms_per_step": round(dta / ksteps * 1e3, 4),
-                               "roofline": roofline_of(doma, PEAK_TFLOPS[dt_acc], committed_traffic(dt_acc)),
-                               "per_layer_ms": pla,
-                               "mpjpe_delta_mm": abs(mp(yas) - mp(ref)) * 1e3,
-                               "max_coord_delta_mm": float(np.abs(yas - ref).max()) * 1e3}
-                parity[f"{dt_acc}_mpjpe_delta_mm"] = out[dt_acc]["mpjpe_delta_mm"]
-                parity[f"{dt_acc}_max_coord_delta_mm"] = out[dt_acc]["max_coord_delta_mm"]
-                del ya
-            if "f16x3" in out:
-                out["f16x3"]["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per "
-                                                        "algorithmic multiply-add (hi.hi + hi.lo + lo.hi)")
-            if not traj:
-                # ---- config-2 batch sweep (1 GPU) ----
-                sweep = {}
-                for Bs in args.sweep:
-                    if Bs == B:
-                        sweep[str(Bs)] = round(value, 2)
-                        continue
-                    ps = torch.from_numpy(pool.global_pairs(Bs)).to(dev)
-                    xsw = pool.seqs.gather(ps, RF, pad, "2d").view(Bs, RF, jin, 2) if args.pregathered else None
-                    ysw = torch.empty((Bs, 1, JOINTS, 3), device=dev)
-                    lifter.reserve(Bs, RF, dtype)
-                    ks = max(5, args.steps // 2)
-                    dts = timed_steps(make_step(dtype, xsw, ps, ysw), ks, 3, 0.2, 1)
-                    sweep[str(Bs)] = round(Bs * ks / dts, 2)
-                    del xsw, ysw
-                out["batch_sweep_poses_per_s"] = sweep
-        # ---- CPU baseline: the oracle (reference op sequence) on 64 windows of the same set ----
+                if Bs == B and sdt in out:
+                    row[str(Bs)] = out[sdt]["value"]
+                    continue
+                ps = torch.from_numpy(case.pool.global_pairs(Bs)).to(dev)
+                ysw = torch.empty((Bs, 1, JOINTS, 3), device=dev)
+                xsw = case.pool.seqs.gather(ps, case.RF, case.pad, "2d").view(Bs, case.RF, case.jin, 2) \
+                    if args.pregathered else None
+                case.lifter.reserve(Bs, case.RF, sdt)
+                ks = max(5, args.steps // 2)
+                with torch.no_grad():
+                    dts = timed_steps(case.make_step(sdt, ysw, ps, xsw), ks, 3, 0.2, 1)
+                row[str(Bs)] = round(Bs * ks / dts, 2)
+                del ysw, xsw
+            sweep[sdt] = row
+        out["batch_sweep_poses_per_s"] = sweep
+    # ---- CPU baseline: the oracle (reference op sequence) on 64 windows of the same set ----
+    if args.cpu_seconds > 0:
+        cpu = case.cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu
+        out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        for dl in legs:
+            if dl in out:
+                out[dl]["speedup_vs_cpu"] = round(out[dl]["value"] / cpu["value"], 1)
+    case.close()
+    del case
+    if not traj and not args.no_legs:
+        # ---- config 3 at the same global batch: fp16 (fast), f16x3 and fp32 (the gate) ----
+        c3 = WindowsCase(True, args.global_batch, 0, 1, dev)
+        leg3 = {"workload": "config3 trajectory-conditioned (46ch: K.E of every frame + window gather + camera "
+                            "concat inside the step) TemporalModelOptimized1f, 243-frame RF windows of the dolly "
+                            "sequences (K.E translations to ~22 m)", "global_batch": c3.G,
+                "flop_per_pose": c3.flop_pose, "parity_info": c3.parity_info(P)}
+        for dl, ks in (("fp16", max(5, args.steps // 2)), ("f16x3", max(5, args.steps // 2)),
+                       ("fp32", max(3, args.steps // 4))):
+            leg3[dl] = c3.leg(dl, ks, 1, 0.3, P)
         if args.cpu_seconds > 0:
-            xc = pool.seqs.gather(pairs[:64].contiguous(), RF, pad, "2d", concat_cams=traj).view(-1, RF, jin, 2).cpu()
-            cpu = cpu_baseline(lambda: lifter_forward(sd, xc, FW, strided=True), int(xc.shape[0]), "poses/s",
-                               f"windows of 243x{jin}x2 through oracle/temporal_ref.py (torch-CPU, fp32, batch "
-                               f"{int(xc.shape[0])})", target_s=args.cpu_seconds / 5)
-            out["cpu_baseline"] = cpu
-            out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
-            for dt_acc in ("fp32", "f16x3"):
-                if dt_acc in out:
-                    out[dt_acc]["speedup_vs_cpu"] = round(out[dt_acc]["value"] / cpu["value"], 1)
+            leg3["cpu_baseline"] = c3.cpu_baseline(args.cpu_seconds)
+            for dl in ("fp16", "f16x3", "fp32"):
+                leg3[dl]["speedup_vs_cpu"] = round(leg3[dl]["value"] / leg3["cpu_baseline"]["value"], 1)
+        out["config3"] = leg3
+        c3.close()
+        del c3
+        # ---- config 5: causal streaming (fp16, hipGraph of 64 steps; serve latency) ----
+        a5 = argparse.Namespace(**vars(args))
+        a5.dtype, a5.steps, a5.warmup = "fp16", 64 * 40, 64 * 4
+        out["config5"] = stream_main(a5, 1, 0, dev, emit=False)
     print(json.dumps(out), flush=True)
 
 

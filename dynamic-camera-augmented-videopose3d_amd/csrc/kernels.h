@@ -204,12 +204,18 @@ struct StreamPipeParams {
     // role stores pose granules the host polls (no fence or done word after them).  The
     // expand role ends the launch at the first frame not posted within idle_ticks (100 MHz
     // clock) or once *stop is set, by writing it to *end_frame (device word, all ones while
-    // serving); every other role leaves when it reaches that frame.
+    // serving); every other role leaves when it reaches that frame.  The expand workgroups
+    // agree on that frame through one claim word (*end_claim, = the stream position at
+    // serve_begin): each commits a frame it took by an atomic max to frame + 1, an ending
+    // workgroup claims frame t by CAS(t -> kServeEndBit | t) -- which fails once any of them
+    // committed t -- and a workgroup whose commit returns an end at or before its frame rolls
+    // that frame back (output granules untagged, history restored)
     int serve;
     const unsigned long long* frame_gran;
     unsigned long long* pose_gran;
     const unsigned* stop;
     unsigned* end_frame;
+    unsigned* end_claim;
     unsigned* ended_host;                  // host-mapped copy of the end frame + 1 (0 while serving)
     unsigned long long idle_ticks;
     // diagnostics (VP3D_STREAM_TRACE=n at vp3d_stream_create): every workgroup records the
@@ -219,6 +225,7 @@ struct StreamPipeParams {
     unsigned long long* trace;
     int trace_frames;
 };
+constexpr unsigned kServeEndBit = 0x80000000u;
 int stream_pipe_lds_bytes(int C, int cin0, int max_ring);
 bool stream_pipe_channels_ok(int C);
 hipError_t stream_pipe_prepare(Act wtype, int C, int lds_bytes);  // dynamic-LDS attribute, once

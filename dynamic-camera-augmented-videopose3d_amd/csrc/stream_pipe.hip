@@ -272,6 +272,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     constexpr int CWK = kPipeCwK, CWP = kPipeCwP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int abort_flag, end_flag;
+    __shared__ int rollback_flag;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wg = blockIdx.x;
     const int C = p.C, nb = p.nb, nl = p.nl, Q = p.queue;
@@ -322,6 +323,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     if (tid == 0) {
         abort_flag = 0;
         end_flag = 0;
+        rollback_flag = 0;
     }
 
     // ---- LDS carve ----
@@ -373,6 +375,8 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         // in LDS only carries them across launches); the padding of both input buffers is
         // written once
         float hp1 = tid < cin0 ? hist[tid] : 0.f, hp2 = tid < cin0 ? hist[cin0 + tid] : 0.f;
+        float ph1 = hp1, ph2 = hp2;  // serve: the history before the last frame taken
+        unsigned claim_old = 0;      // serve, thread 0: what the commit of the last frame returned
         for (int i = 3 * cin0 + tid; i < 2 * kPipeExpandK; i += kThreads)
             if (i % kPipeExpandK >= 3 * cin0) xin[i] = 0.f;
         for (int s = 0;; ++s) {
@@ -382,13 +386,21 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 if (s >= p.steps) break;
                 if (tid < cin0) fv = p.frames[(int64_t)(t & (Q - 1)) * cin0 + tid];
             } else {
+                // frame t - 1 was taken speculatively: its commit returned an end at or before
+                // it -> another expand workgroup ended the launch there (roll t - 1 back below;
+                // the commit was issued a frame ago, so this read rarely waits)
+                if (tid == 0 && s > 0 && (claim_old & kServeEndBit) && (claim_old & ~kServeEndBit) <= (unsigned)t - 1u) {
+                    rollback_flag = 1;
+                    end_flag = 1;
+                }
                 // serve: thread i < cin0 polls granule i of frame t in the host ring (one PCIe
                 // round trip brings the value with its tag); thread 0 also ends the launch on a
-                // stop request or after idle_ticks without the frame
+                // stop request or after idle_ticks without the frame -- if it can claim frame t
+                // as the end (no expand workgroup committed t)
                 if (tid < cin0) {
                     // (the barrier below also publishes end_flag)
                     const gu64* fg = (const gu64*)p.frame_gran + (int64_t)(t & (Q - 1)) * cin0 + tid;
-                    const unsigned long long start = __builtin_amdgcn_s_memrealtime();
+                    unsigned long long start = __builtin_amdgcn_s_memrealtime();
                     for (;;) {
                         const unsigned long long x = __hip_atomic_load(fg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         if ((unsigned)(x >> 32) == (unsigned)t + 1u) {
@@ -402,16 +414,32 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                                 (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
                                  now - start > p.idle_ticks)) {
                                 // the host writes a frame's granules before a stop request: a
-                                // granule still missing now means frame t was never posted
+                                // granule still missing now means frame t was not posted in time
                                 const unsigned long long y = __hip_atomic_load(fg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                                 if ((unsigned)(y >> 32) == (unsigned)t + 1u) {
                                     fv = __uint_as_float((unsigned)y);
                                     break;
                                 }
-                                __hip_atomic_store(p.end_frame, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                __hip_atomic_store(p.ended_host, (unsigned)t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                                __hip_atomic_store(&end_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                                break;
+                                unsigned expect = (unsigned)t;
+                                if (__hip_atomic_compare_exchange_strong(p.end_claim, &expect, kServeEndBit | (unsigned)t,
+                                                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                                    // frame t is the end: no expand workgroup took it, and none will
+                                    __hip_atomic_store(p.end_frame, (unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    __hip_atomic_store(p.ended_host, (unsigned)t + 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                                    __hip_atomic_store(&end_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    break;
+                                }
+                                if ((expect & kServeEndBit) && (expect & ~kServeEndBit) <= (unsigned)t) {
+                                    // another expand workgroup claimed the end at this frame
+                                    __hip_atomic_store(&end_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    break;
+                                }
+                                // another expand workgroup committed frame t (the whole frame was
+                                // posted): it arrives, keep polling; the next end check after another
+                                // idle period
+                                start = now;
                             }
                         }
                         __builtin_amdgcn_s_sleep(1);
@@ -434,9 +462,25 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 nh1 = v;
             }
             __syncthreads();
-            if (p.serve && end_flag) break;  // frame t was never posted: the history stays
+            if (p.serve && end_flag) {
+                // frame t was never posted: the history stays; a rolled-back frame t - 1 leaves
+                // no trace (history as before it, its output granules untagged)
+                if (rollback_flag) {
+                    hp1 = ph1;
+                    hp2 = ph2;
+                    if (c < c_hi) publish(out_at(0, t - 1, c), 0u, 0.f);
+                }
+                break;
+            }
+            ph1 = hp1;
+            ph2 = hp2;
             hp1 = nh1;
             hp2 = nh2;
+            // serve: commit frame t (speculatively: its outputs go out before the answer,
+            // checked at the next frame)
+            if (p.serve && tid == 0)
+                claim_old = __hip_atomic_fetch_max(p.end_claim, (unsigned)t + 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
             trace_mark(p, wg, s, 0, tid);
             if (c < c_hi) {
                 // four independent chains (two v_pk_fma_f32 chains; a 128-deep dependent chain

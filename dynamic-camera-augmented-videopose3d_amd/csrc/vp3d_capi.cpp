@@ -562,6 +562,9 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
             e = launch_conv_gemm(p, Act::F32, Act::F32, Act::F32, s);
             launched = true;
         } else if (x3 && first && nl > 2 && [&] {
+                       // VP3D_X3_EXPAND=pack (measurement): the pack + GEMM form instead
+                       const char* xe = getenv("VP3D_X3_EXPAND");
+                       if (xe && strcmp(xe, "pack") == 0) return false;
                        ConvGemmParams q = p;
                        q.W = L.wx3;
                        q.Kp = 2 * L.Kp;
@@ -1169,7 +1172,8 @@ int vp3d_stream_reset(vp3d_stream* st, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     if (st->serving) return fail(VP3D_ERR_STATE, "serving: vp3d_stream_serve_end first");
     // position, arrival counter and the sticky timeout word; the host mirror is cleared
-    // once no launch of this stream can still set it
+    // once no launch of this stream can still set it (launches may have gone to any stream)
+    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemsetAsync(st->frames_seen, 0, 16, (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     *(volatile unsigned*)st->err_host = 0u;
@@ -1289,7 +1293,7 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     if (!st->serve_host) {
         HIP_TRY(hipHostMalloc(&st->serve_host, bytes, hipHostMallocMapped));
         HIP_TRY(hipHostGetDevicePointer(&st->serve_dev, st->serve_host, 0));
-        HIP_TRY(hipMalloc(&st->end_frame, 4));
+        HIP_TRY(hipMalloc(&st->end_frame, 8));  // [0] end frame, [1] the expand role's claim word
     }
     // the stream position of the device (any earlier launches on `stream` finished)
     HIP_TRY(hipStreamSynchronize(s));
@@ -1300,7 +1304,8 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     st->done_seen = pos;
     // no granule of an earlier session (or of frames before a reset) may carry a tag of this one
     std::memset(st->serve_host, 0, bytes);
-    HIP_TRY(hipMemsetAsync(st->end_frame, 0xff, 4, s));
+    const unsigned ctl[2] = {0xFFFFFFFFu, (unsigned)pos};  // not ended; frames before pos committed
+    HIP_TRY(hipMemcpy(st->end_frame, ctl, 8, hipMemcpyHostToDevice));
     StreamPipeParams p = st->pipe_p;
     p.serve = 1;
     p.frame_gran = (const unsigned long long*)dev_view(st, serve_frames(st));
@@ -1308,6 +1313,7 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     p.stop = dev_view(st, serve_ctrl(st) + 1);
     p.ended_host = dev_view(st, serve_ctrl(st) + 2);
     p.end_frame = st->end_frame;
+    p.end_claim = st->end_frame + 1;
     p.idle_ticks = (unsigned long long)(idle_ms * 1e5);  // 100 MHz clock
     p.steps = 0;
     const Act wt = st->dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16;
@@ -1379,7 +1385,9 @@ int vp3d_stream_serve_end(vp3d_stream* st, void* stream) {
     if (!st->serving) return VP3D_OK;
     __atomic_store_n(serve_ctrl(st) + 1, 1u, __ATOMIC_RELEASE);
     st->serving = false;
-    HIP_TRY(hipStreamSynchronize(stream ? (hipStream_t)stream : st->serve_stream));
+    // the resident launch runs on the stream serve_begin was given, whatever `stream` is
+    (void)stream;
+    HIP_TRY(hipStreamSynchronize(st->serve_stream));
     int pos = 0;
     HIP_TRY(hipMemcpy(&pos, st->frames_seen, 4, hipMemcpyDeviceToHost));
     st->host_t = pos;

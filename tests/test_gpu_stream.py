@@ -184,3 +184,48 @@ def test_stream_serve_one_frame_in_flight():
         with pytest.raises(RuntimeError, match="ended"):
             sv.post(x[0, 65])
     assert st.frames_seen() == 65
+
+
+def test_stream_serve_restarts_at_the_idle_limit():
+    """A frame posted right at the idle limit: the launch's expand workgroups (4 at 1024
+    channels) agree on one end frame (the claim word of stream_pipe.hip), so whichever way
+    each race goes the stream position never skips a frame and the expand histories stay in
+    step.  Frames are posted with delays around idle_ms; every time the launch has ended
+    the session is restarted at the device's position and the frame re-posted.  The poses
+    of all frames must equal the batch form's bit for bit."""
+    import time
+    fw = (3, 3, 3, 3, 3)
+    m, sd = make_model(False, fw, causal=True)
+    T = 64
+    x = synth.normalized_windows(23, "stream_serve_edge", 1, T)
+    m.cuda()
+    st = CausalStream(m.native_lifter(), "fp16")
+    rng = np.random.default_rng(5)
+    idle_ms = 0.1
+    poses = {}
+    restarts = 0
+    t = 0
+    while t < T:
+        with st.serve(idle_ms=idle_ms) as sv:
+            assert st.frames_seen() == t
+            while t < T:
+                deadline = time.perf_counter() + rng.uniform(0.06e-3, 0.14e-3)
+                while time.perf_counter() < deadline:
+                    pass
+                try:
+                    i = sv.post(x[0, t])
+                    assert i == t
+                    poses[t] = sv.wait(t)
+                except RuntimeError as e:
+                    assert "ended" in str(e), e
+                    break
+                t += 1
+        restarts += 1
+        t = st.frames_seen()
+        assert sorted(poses) == list(range(t)), (t, sorted(poses)[-3:])  # no frame skipped or repeated
+    print(f"serve at the idle edge: {restarts} sessions for {T} frames")
+    assert restarts > 1
+    st.reset()
+    xs = torch.from_numpy(x[0]).cuda()
+    batch = torch.stack([st.step(xs[k]).clone() for k in range(T)]).cpu().numpy()
+    np.testing.assert_array_equal(np.stack([poses[k] for k in range(T)]), batch)

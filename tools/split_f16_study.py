@@ -143,6 +143,12 @@ def main():
     print(f"split vs fp32 oracle: max {np.abs(y - ref).max() * 1e3:.3e} mm  dMPJPE {abs(mp(y) - mp(ref)) * 1e3:.3e} mm")
     print(f"split vs f64:         max {np.abs(y - ref64).max() * 1e3:.3e} mm  dMPJPE {abs(mp(y) - mp(ref64)) * 1e3:.3e} mm")
     print(f"fp32 oracle vs f64:   max {np.abs(ref - ref64).max() * 1e3:.3e} mm  dMPJPE {abs(mp(ref) - mp(ref64)) * 1e3:.3e} mm")
+    r64 = ref64.astype(np.float64)
+    rr = float(np.sum(r64 * r64))
+    for name, v in (("split", y), ("fp32 oracle", ref)):
+        d = v.astype(np.float64) - r64
+        print(f"{name:12s} vs f64: scale eps {np.sum(d * r64) / rr * 2 ** 24:+.2f} x 2^-24, "
+              f"rms {np.sqrt(np.sum(d * d) / rr) * 2 ** 24:.2f} x 2^-24")
 
 
 if __name__ == "__main__":

@@ -86,7 +86,16 @@ def main():
         wr = 1024.0 * sum(w) / len(w)
         per_layer[layer] = {"read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
                             "launches": min(len(f), len(w))}
+    import subprocess
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "dynamic-camera-augmented-videopose3d_amd"))
+    from vp3d_amd import build as _build
+    try:
+        commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    except OSError:
+        commit = None
     out = {"batch": a.batch, "dtype": a.dtype, "dominant": a.dominant,
+           "build_hash": _build.source_hash(), "git_commit": commit or None,
            "hbm_bytes_per_launch": per_layer.get(a.dominant, {}).get("hbm_bytes"),
            "per_layer": per_layer,
            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes in {a.dir}/{a.prefix}*; "

@@ -19,11 +19,13 @@
 //
 //   hipcc --offload-arch=gfx950 -O2 -o tools/ubench/mfma_bias tools/ubench/mfma_bias.hip
 //   tools/ubench/mfma_bias [K] [tiles] [dist]
+//   tools/ubench/mfma_bias file A.bin W.bin M N K     (real operands: tools/real_operands.py)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -43,13 +45,16 @@ struct Ops {
     const float *a, *w;                 // f32 values (W already scaled)
     float* out;                         // [tile][256]
     int K, mode, L;
+    int tn;  // 0: tile t pairs A tile t with W tile t; else A tile t / tn with W tile t % tn
 };
 
 __device__ __forceinline__ f16x8 ld8(const _Float16* p) { return *(const f16x8*)p; }
 
 __global__ __launch_bounds__(64) void chain(Ops o) {
     const int lane = threadIdx.x, t = blockIdx.x;
-    const size_t base = (size_t)t * 16 * o.K + (size_t)(lane & 15) * o.K + 8 * (lane >> 4);
+    const int at = o.tn ? t / o.tn : t, wt = o.tn ? t % o.tn : t;
+    const size_t abase = (size_t)at * 16 * o.K + (size_t)(lane & 15) * o.K + 8 * (lane >> 4);
+    const size_t wbase = (size_t)wt * 16 * o.K + (size_t)(lane & 15) * o.K + 8 * (lane >> 4);
     const int steps = o.K / 32;
     f32x4 acc = {0, 0, 0, 0}, x = {0, 0, 0, 0}, m = {0, 0, 0, 0};
     float res[4];
@@ -57,16 +62,16 @@ __global__ __launch_bounds__(64) void chain(Ops o) {
         // lane (l & 15, l >> 4) owns outputs n = 4 (l >> 4) + r, row m = l & 15
         for (int r = 0; r < 4; ++r) {
             const int n = 4 * (lane >> 4) + r, mm = lane & 15;
-            const float* wr = o.w + (size_t)t * 16 * o.K + (size_t)n * o.K;
-            const float* ar = o.a + (size_t)t * 16 * o.K + (size_t)mm * o.K;
+            const float* wr = o.w + (size_t)wt * 16 * o.K + (size_t)n * o.K;
+            const float* ar = o.a + (size_t)at * 16 * o.K + (size_t)mm * o.K;
             float s = 0.f;
             for (int k = 0; k < o.K; ++k) s = fmaf(wr[k], ar[k], s);
             res[r] = s;
         }
     } else {
         for (int s = 0; s < steps; ++s) {
-            const size_t off = base + 32 * s;
-            const f16x8 Ah = ld8(o.ah + off), Al = ld8(o.al + off), Wh = ld8(o.wh + off), Wl = ld8(o.wl + off);
+            const size_t ao = abase + 32 * s, wo = wbase + 32 * s;
+            const f16x8 Ah = ld8(o.ah + ao), Al = ld8(o.al + ao), Wh = ld8(o.wh + wo), Wl = ld8(o.wl + wo);
             switch (o.mode) {
                 case 0:
                     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh, Ah, acc, 0, 0, 0);
@@ -134,68 +139,101 @@ static double urand() {
 }
 static double nrand() { return std::sqrt(-2.0 * std::log(urand())) * std::cos(6.283185307179586 * urand()); }
 
+static std::vector<float> read_f32(const char* path, size_t n) {
+    std::vector<float> v(n);
+    FILE* f = fopen(path, "rb");
+    if (!f || fread(v.data(), 4, n, f) != n) {
+        fprintf(stderr, "cannot read %zu floats from %s\n", n, path);
+        exit(1);
+    }
+    fclose(f);
+    return v;
+}
+
 int main(int argc, char** argv) {
-    const int K = argc > 1 ? atoi(argv[1]) : 3072;
-    const int T = argc > 2 ? atoi(argv[2]) : 512;
-    const int dist = argc > 3 ? atoi(argv[3]) : 0;
-    const size_t n = (size_t)T * 16 * K;
-    std::vector<float> a(n), w(n);
-    std::vector<_Float16> ah(n), al(n), wh(n), wl(n);
-    for (int t = 0; t < T; ++t) {
-        double wmax = 0;
-        for (int r = 0; r < 16; ++r) {
-            // dist 0: A = relu(N(0,1)); dist 1: per-row scale 2^U(-4,4), relu(N(0.3,1));
-            // dist 2: as 1 with 1/8 of the K values 20x larger (metre-scale camera channels)
-            const double rsc = dist == 0 ? 1.0 : std::exp2(8.0 * urand() - 4.0);
-            for (int k = 0; k < K; ++k) {
-                const size_t i = ((size_t)t * 16 + r) * K + k;
-                double v = std::max(0.0, nrand() + (dist == 0 ? 0.0 : 0.3)) * rsc;
-                if (dist == 2 && (k % 8) == 0) v *= 20.0;
-                a[i] = (float)v;
-                w[i] = (float)(nrand() / std::sqrt((double)K));
-                wmax = std::max(wmax, (double)std::fabs(w[i]));
-            }
-        }
-        const int e = 14 - (int)std::floor(std::log2(wmax));
-        for (int r = 0; r < 16; ++r)
-            for (int k = 0; k < K; ++k) {
-                const size_t i = ((size_t)t * 16 + r) * K + k;
-                w[i] = std::ldexp(w[i], e);
-                ah[i] = (_Float16)a[i];
-                al[i] = (_Float16)(a[i] - (float)ah[i]);
-                wh[i] = (_Float16)w[i];
-                wl[i] = (_Float16)(w[i] - (float)wh[i]);
+    // synthetic: mfma_bias [K] [tiles] [dist];  real operands: mfma_bias file A.bin W.bin M N K
+    const bool file = argc > 1 && std::string(argv[1]) == "file";
+    int K, T, dist = 0, M = 0, NW = 0, tn = 0;
+    std::vector<float> a, w;
+    if (file) {
+        M = atoi(argv[4]);
+        NW = atoi(argv[5]);
+        K = atoi(argv[6]);
+        a = read_f32(argv[2], (size_t)M * K);
+        w = read_f32(argv[3], (size_t)NW * K);
+        T = (M / 16) * (NW / 16);
+        tn = NW / 16;
+    } else {
+        K = argc > 1 ? atoi(argv[1]) : 3072;
+        T = argc > 2 ? atoi(argv[2]) : 512;
+        dist = argc > 3 ? atoi(argv[3]) : 0;
+    }
+    const size_t na = file ? (size_t)M * K : (size_t)T * 16 * K, nw = file ? (size_t)NW * K : (size_t)T * 16 * K;
+    if (!file) {
+        a.resize(na);
+        w.resize(nw);
+    }
+    std::vector<_Float16> ah(na), al(na), wh(nw), wl(nw);
+    if (!file) {
+        for (int t = 0; t < T; ++t)
+            for (int r = 0; r < 16; ++r) {
+                // dist 0: A = relu(N(0,1)); dist 1: per-row scale 2^U(-4,4), relu(N(0.3,1));
+                // dist 2: as 1 with 1/8 of the K values 20x larger (metre-scale camera channels)
+                const double rsc = dist == 0 ? 1.0 : std::exp2(8.0 * urand() - 4.0);
+                for (int k = 0; k < K; ++k) {
+                    const size_t i = ((size_t)t * 16 + r) * K + k;
+                    double v = std::max(0.0, nrand() + (dist == 0 ? 0.0 : 0.3)) * rsc;
+                    if (dist == 2 && (k % 8) == 0) v *= 20.0;
+                    a[i] = (float)v;
+                    w[i] = (float)(nrand() / std::sqrt((double)K));
+                }
             }
     }
+    // weights scaled by 2^e, max |W 2^e| in [2^14, 2^15) (the library's split weights: per layer;
+    // here per operand set)
+    double wmax = 0;
+    for (float v : w) wmax = std::max(wmax, (double)std::fabs(v));
+    const int e = 14 - (int)std::floor(std::log2(wmax));
+    for (size_t i = 0; i < nw; ++i) {
+        w[i] = std::ldexp(w[i], e);
+        wh[i] = (_Float16)w[i];
+        wl[i] = (_Float16)(w[i] - (float)wh[i]);
+    }
+    for (size_t i = 0; i < na; ++i) {
+        ah[i] = (_Float16)a[i];
+        al[i] = (_Float16)(a[i] - (float)ah[i]);
+    }
     // exact sums (float64 of the f32 operand products; and of Wh.Ah for mode 5)
-    std::vector<double> ex(T * 256), exh(T * 256);
-    for (int t = 0; t < T; ++t)
+    std::vector<double> ex((size_t)T * 256), exh((size_t)T * 256);
+    for (int t = 0; t < T; ++t) {
+        const int at = tn ? t / tn : t, wt = tn ? t % tn : t;
         for (int nn = 0; nn < 16; ++nn)
             for (int mm = 0; mm < 16; ++mm) {
                 double s = 0, sh = 0;
-                const size_t wr = ((size_t)t * 16 + nn) * K, ar = ((size_t)t * 16 + mm) * K;
+                const size_t wr = ((size_t)wt * 16 + nn) * K, ar = ((size_t)at * 16 + mm) * K;
                 for (int k = 0; k < K; ++k) {
                     s += (double)w[wr + k] * (double)a[ar + k];
                     sh += (double)wh[wr + k] * (double)ah[ar + k];
                 }
-                ex[t * 256 + nn * 16 + mm] = s;
-                exh[t * 256 + nn * 16 + mm] = sh;
+                ex[(size_t)t * 256 + nn * 16 + mm] = s;
+                exh[(size_t)t * 256 + nn * 16 + mm] = sh;
             }
+    }
     _Float16 *dah, *dal, *dwh, *dwl;
     float *da, *dw, *dout;
-    CHECK(hipMalloc(&dah, n * 2));
-    CHECK(hipMalloc(&dal, n * 2));
-    CHECK(hipMalloc(&dwh, n * 2));
-    CHECK(hipMalloc(&dwl, n * 2));
-    CHECK(hipMalloc(&da, n * 4));
-    CHECK(hipMalloc(&dw, n * 4));
+    CHECK(hipMalloc(&dah, na * 2));
+    CHECK(hipMalloc(&dal, na * 2));
+    CHECK(hipMalloc(&dwh, nw * 2));
+    CHECK(hipMalloc(&dwl, nw * 2));
+    CHECK(hipMalloc(&da, na * 4));
+    CHECK(hipMalloc(&dw, nw * 4));
     CHECK(hipMalloc(&dout, (size_t)T * 256 * 4));
-    CHECK(hipMemcpy(dah, ah.data(), n * 2, hipMemcpyHostToDevice));
-    CHECK(hipMemcpy(dal, al.data(), n * 2, hipMemcpyHostToDevice));
-    CHECK(hipMemcpy(dwh, wh.data(), n * 2, hipMemcpyHostToDevice));
-    CHECK(hipMemcpy(dwl, wl.data(), n * 2, hipMemcpyHostToDevice));
-    CHECK(hipMemcpy(da, a.data(), n * 4, hipMemcpyHostToDevice));
-    CHECK(hipMemcpy(dw, w.data(), n * 4, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dah, ah.data(), na * 2, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dal, al.data(), na * 2, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dwh, wh.data(), nw * 2, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dwl, wl.data(), nw * 2, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(da, a.data(), na * 4, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dw, w.data(), nw * 4, hipMemcpyHostToDevice));
     struct Cfg {
         const char* name;
         int mode, L;
@@ -204,23 +242,27 @@ int main(int argc, char** argv) {
                 {"flush L=32", 2, 32},         {"two chains", 3, 1},              {"fmaf chain (f32)", 4, 1},
                 {"hh only vs exact hh", 5, 1}, {"mfma-flush L=4", 6, 4},          {"mfma-flush L=8", 6, 8}};
     std::vector<float> out((size_t)T * 256), out_flush4;
-    printf("K=%d tiles=%d dist=%d outputs=%d (units: 2^-24 relative)\n", K, T, dist, T * 256);
+    if (file)
+        printf("file operands: M=%d N=%d K=%d outputs=%d (units: 2^-24 relative)\n", M, NW, K, T * 256);
+    else
+        printf("K=%d tiles=%d dist=%d outputs=%d (units: 2^-24 relative)\n", K, T, dist, T * 256);
     for (const Cfg& c : cfgs) {
-        Ops o{dah, dal, dwh, dwl, da, dw, dout, K, c.mode, c.L};
+        Ops o{dah, dal, dwh, dwl, da, dw, dout, K, c.mode, c.L, tn};
         hipLaunchKernelGGL(chain, dim3(T), dim3(64), 0, 0, o);
         CHECK(hipGetLastError());
         CHECK(hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost));
         const std::vector<double>& E = c.mode == 5 ? exh : ex;
-        double sb = 0, s2 = 0, sa = 0, sa2 = 0, mx = 0;
+        double sb = 0, s2 = 0, sa = 0, sa2 = 0, se = 0;
         for (size_t i = 0; i < out.size(); ++i) {
             const double d = (double)out[i] - E[i];
             sb += d * (E[i] > 0 ? 1 : -1);
             sa += std::fabs(E[i]);
             s2 += d * d;
             sa2 += E[i] * E[i];
-            mx = std::max(mx, std::fabs(d) / std::max(std::fabs(E[i]), 1e-30));
+            se += d * E[i];
         }
-        printf("%-26s bias %+8.4f  rms %8.4f  (x 2^-24)\n", c.name, sb / sa * 0x1p24, std::sqrt(s2 / sa2) * 0x1p24);
+        printf("%-26s bias %+8.4f  eps %+8.4f  rms %8.4f  (x 2^-24)\n", c.name, sb / sa * 0x1p24, se / sa2 * 0x1p24,
+               std::sqrt(s2 / sa2) * 0x1p24);
         if (c.mode == 2 && c.L == 4) out_flush4 = out;
         if (c.mode == 6 && c.L == 4) {
             size_t diff = 0;
