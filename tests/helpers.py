@@ -5,12 +5,12 @@ import torch
 from vp3d_amd import synth
 
 
-# 16-bit gates: (max |coordinate delta|, |dMPJPE|) in metres, about 3x the largest error
-# measured on MI355X over the lifter tests (round 2: bf16 3.56 mm max on the dilated
-# 20,242-frame sequence, 0.057 mm dMPJPE; fp16 0.35 mm at B = 2050, 0.0058 mm), on outputs
-# of ~0.11 m rms (synth.normalized_windows inputs): bf16 ~ 9e-2 x rms, fp16 ~ 1.1e-2 x rms.
+# 16-bit gates: (max |coordinate delta|, |dMPJPE|) in metres, 1.6-3x the largest error measured
+# on MI355X over the lifter tests (round 4, profiles/r04j_pytest_traj_golden_lifter.txt: bf16
+# 3.77 mm max on the dilated 20,242-frame sequence, 0.062 mm dMPJPE; fp16 0.37 mm, 0.0074 mm),
+# on outputs of ~0.11 m rms (synth.normalized_windows inputs).
 H16_TOL = {
-    "bf16": (1.0e-2, 1.5e-4),
+    "bf16": (6.0e-3, 1.25e-4),
     "fp16": (1.2e-3, 2.0e-5),
 }
 
