@@ -131,7 +131,7 @@ __device__ __forceinline__ float aread() {
 __device__ unsigned long long* g_a4_trace;
 #endif
 
-template <typename CT, int ABL, int X3 = 0>
+template <typename CT, int ABL, int X3 = 0, bool GD = true>
 __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     // the accumulator file is this kernel's own from here on (see the header)
     asm volatile("" ::: A4_ALL_AGPRS);
@@ -188,6 +188,12 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     // shape, B = 8192, 1.251-1.262 vs 1.231-1.237 ms) ----
     int prow = lane >> 3;
     int lc = (lane & 7) ^ (((wid & 1) * 4 + (prow >> 1)) & 7);
+    // GD (grouped pieces): wave w's 8 A pieces are the consecutive slots 8w .. 8w + 7 (tile rows
+    // 64w .. 64w + 63; W likewise), issued as 2 groups of 4 that share one LDS base (M0) and
+    // differ by the instruction offset (i & 3) KiB -- applied to the LDS and the global address
+    // alike, so the lane offsets carry - (i & 3) KiB against resources based 3 KiB early.  One
+    // M0 write per 4 pieces instead of one per piece.  Otherwise slot w + 4i, M0 per piece.
+    constexpr int kReb = GD ? 3072 : 0;
     int m0 = 0, n0 = 0;
     uint32_t va[8], vw[8], vr[8];
     __amdgpu_buffer_rsrc_t a_rsrc, w_rsrc, r_rsrc;
@@ -198,17 +204,21 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         m0 = tile_m * GM;
         n0 = tile_n * GN;
         const int srow0 = src_row(p, m0);  // m0 < M; wave-uniform
-        a_rsrc = make_rsrc((const CT*)p.A + (int64_t)srow0 * p.lda, 0x7FFFFFFFu);
-        w_rsrc = make_rsrc((const CT*)p.W + (int64_t)n0 * p.Kp, 0x7FFFFFFFu);
+        a_rsrc = make_rsrc((const char*)((const CT*)p.A + (int64_t)srow0 * p.lda) - kReb, 0x7FFFFFFFu);
+        w_rsrc = make_rsrc((const char*)((const CT*)p.W + (int64_t)n0 * p.Kp) - kReb, 0x7FFFFFFFu);
         const int rrow0 = lres ? res_row(p, m0) : 0;
-        r_rsrc = make_rsrc(lres ? (const CT*)p.R + (int64_t)rrow0 * p.ldr : (const CT*)p.A, 0x7FFFFFFFu);
+        r_rsrc = make_rsrc((const char*)(lres ? (const CT*)p.R + (int64_t)rrow0 * p.ldr : (const CT*)p.A) - kReb,
+                           0x7FFFFFFFu);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            int m = m0 + 8 * (wid + 4 * i) + prow;
+            const int q = GD ? 8 * wid + i : wid + 4 * i;  // the piece's slot: rows 8q .. 8q + 7
+            const int lci = GD ? (lane & 7) ^ (((i & 1) * 4 + (prow >> 1)) & 7) : lc;
+            const int reb = GD ? kReb - (i & 3) * 1024 : 0;
+            int m = m0 + 8 * q + prow;
             m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
-            va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lc * 8) * (int)sizeof(CT));
-            vw[i] = (uint32_t)(((8 * (wid + 4 * i) + prow) * p.Kp + lc * 8) * (int)sizeof(CT));  // W rows padded
-            vr[i] = lres ? (uint32_t)(((res_row(p, m) - rrow0) * p.ldr + lc * 8) * (int)sizeof(CT)) : 0u;
+            va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lci * 8) * (int)sizeof(CT) + reb);
+            vw[i] = (uint32_t)(((8 * q + prow) * p.Kp + lci * 8) * (int)sizeof(CT) + reb);  // W rows padded
+            vr[i] = lres ? (uint32_t)(((res_row(p, m) - rrow0) * p.ldr + lci * 8) * (int)sizeof(CT) + reb) : 0u;
         }
     };
     // piece k of residual part h: wave column k >> 3, the rows of A piece k & 7
@@ -220,10 +230,34 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         launder_s(w);
         return buf + (w + q) * 1024;
     };
-    auto res_piece = [&](char* buf, int k, int h) __attribute__((always_inline)) {
-        const int wcp = k >> 3;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r_rsrc, (lds_ptr_t)lds_dst(buf, wcp * 32 + 4 * (k & 7)), 16, vr[k & 7],
-                                                 (uint32_t)((n0 + 128 * wcp + 64 * h) * (int)sizeof(CT)), 0, 0);
+    // GD: the LDS bases (M0) of this wave's piece groups in a 64 KiB buffer -- A pieces 0-3, 4-7,
+    // W pieces 0-3, 4-7 -- computed once per phase (one laundered wave id), so the compiler can
+    // keep M0 across a group's 4 pieces
+    struct Bases {
+        char* g[4];
+    };
+    auto bases_of = [&](char* buf) __attribute__((always_inline)) -> Bases {
+        int w = widu;
+        launder_s(w);
+        char* b = buf + 8 * w * 1024;
+        return Bases{{b, b + 4096, b + GW_OFF, b + GW_OFF + 4096}};
+    };
+    auto piece_lds = [&](char* buf, int i) __attribute__((always_inline)) -> char* {
+        if constexpr (GD) {
+            int w = widu;
+            launder_s(w);
+            return buf + (8 * w + (i & 4)) * 1024;
+        } else {
+            return lds_dst(buf, 4 * i);
+        }
+    };
+    // (piece indices as integral constants: the instruction offset is an immediate)
+    auto res_piece = [&](char* buf, auto k_c, int h) __attribute__((always_inline)) {
+        constexpr int k = decltype(k_c)::value;
+        constexpr int wcp = k >> 3;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r_rsrc, (lds_ptr_t)piece_lds(buf + wcp * 32 * 1024, k & 7), 16,
+                                                 vr[k & 7], (uint32_t)((n0 + 128 * wcp + 64 * h) * (int)sizeof(CT)),
+                                                 GD ? (k & 3) * 1024 : 0, 0);
     };
     // k offset of K-tile s inside a row: tap * dil rows + channel base (wave-uniform)
     auto a_koff = [&](int s) __attribute__((always_inline)) -> int64_t {
@@ -231,25 +265,27 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         const int tap = k0 / p.Ktap;
         return (int64_t)tap * p.dil * p.lda + (k0 - tap * p.Ktap);
     };
-    auto dma_piece = [&](char* buf, int i, int s, int64_t aoff) __attribute__((always_inline)) {
-        if (i < 8)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)lds_dst(buf, 4 * i), 16, va[i],
-                                                     (uint32_t)aoff * (uint32_t)sizeof(CT), 0, 0);
+    auto dma_piece = [&](char* buf, auto i_c, int s, int64_t aoff, const Bases& bs) __attribute__((always_inline)) {
+        constexpr int i = decltype(i_c)::value;
+        char* const ldsp = GD ? bs.g[i >> 2] : (i < 8 ? lds_dst(buf, 4 * i) : lds_dst(buf + GW_OFF, 4 * (i - 8)));
+        if constexpr (i < 8)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr_t)ldsp, 16, va[i],
+                                                     (uint32_t)aoff * (uint32_t)sizeof(CT), GD ? (i & 3) * 1024 : 0, 0);
         else
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)lds_dst(buf + GW_OFF, 4 * (i - 8)), 16, vw[i - 8],
-                                                     (uint32_t)(s * GK * (int)sizeof(CT)), 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)ldsp, 16, vw[i - 8],
+                                                     (uint32_t)(s * GK * (int)sizeof(CT)), GD ? (i & 3) * 1024 : 0, 0);
     };
     char* const buf0 = smem;
     char* const buf1 = smem + GBUF;
     // K-tiles 0 and 1 of the current tile into buffers 0 and 1
     auto stage_01 = [&]() __attribute__((always_inline)) {
         const int64_t o0 = a_koff(0);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dma_piece(buf0, i, 0, o0);
+        const Bases b0 = bases_of(buf0);
+        static_for<16>([&](auto i_c) __attribute__((always_inline)) { dma_piece(buf0, i_c, 0, o0, b0); });
         if (nk > 1) {
             const int64_t o1 = a_koff(1);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) dma_piece(buf1, i, 1, o1);
+            const Bases b1 = bases_of(buf1);
+            static_for<16>([&](auto i_c) __attribute__((always_inline)) { dma_piece(buf1, i_c, 1, o1, b1); });
         }
     };
 
@@ -274,6 +310,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         constexpr bool RD = decltype(rd_c)::value;
         constexpr bool DMA = decltype(dma_c)::value;
         const int64_t aoff = DMA ? a_koff(s) : 0;
+        const Bases bs = DMA ? bases_of(dbuf) : Bases{};
         // each row block: the MFMA on channel block j, with one memory instruction ahead of
         // the even ones: A read, DMA piece, W read, DMA piece (bursts of 2 reads + 2 pieces
         // at the row block's start measured 3 % slower at B = 8192, the same at 65,536;
@@ -287,9 +324,10 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 constexpr int J = decltype(j_c)::value;
                 if constexpr (DO_RD && J == 0) fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
                 if constexpr (DO_RD && J == 4) fw[NXT][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo);
-                if constexpr (DO_DMA && (J == 2 || J == 6)) dma_piece(dbuf, 2 * I + J / 4, s, aoff);
+                if constexpr (DO_DMA && (J == 2 || J == 6))
+                    dma_piece(dbuf, std::integral_constant<int, 2 * I + J / 4>{}, s, aoff, bs);
                 if constexpr (!DMA && (J == 2 || J == 6)) {
-                    if (resp >= 0) res_piece(dbuf, 2 * I + J / 4, resp);
+                    if (resp >= 0) res_piece(dbuf, std::integral_constant<int, 2 * I + J / 4>{}, resp);
                 }
                 amma<CT, 4 * (8 * I + J), ZERO>(fw[CUR][J], fa[CUR][I]);
                 __builtin_amdgcn_sched_barrier(0);
@@ -468,6 +506,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 constexpr bool DO_RD = decltype(rd_c)::value && !(ABL & 2);
                 constexpr bool DO_DMA = decltype(dma_c)::value && !(ABL & 1);
                 const int64_t aoff = DO_DMA ? a_koff(s) : 0;
+                const Bases bs = DO_DMA ? bases_of(dbuf) : Bases{};
                 static_for<8>([&](auto i_c) __attribute__((always_inline)) {
                     constexpr int I = decltype(i_c)::value;
                     static_for<8>([&](auto j_c) __attribute__((always_inline)) {
@@ -481,13 +520,14 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                         } else if constexpr (KIND == 1) {
                             if constexpr (DO_RD && J == 0 && I > 0)
                                 fa[1 - H][I - 1] = *(const u32x4*)(rbuf + a_base + (I - 1) * 2048 + fo0);
-                            if constexpr (DO_DMA && J == 4) dma_piece(dbuf, I, s, aoff);
+                            if constexpr (DO_DMA && J == 4) dma_piece(dbuf, i_c, s, aoff, bs);
                             amma<CT, 4 * (8 * I + J), false>(fw[0][J], fa[1 - H][I]);
                         } else {
                             if constexpr (DO_RD && J == 0 && I == 0)
                                 fa[1 - H][7] = *(const u32x4*)(rbuf + a_base + 7 * 2048 + fo0);
                             if constexpr (DO_RD && J == 4) fw[0][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo0);
-                            if constexpr (DO_DMA && J == 2) dma_piece(dbuf, 8 + I, s, aoff);
+                            if constexpr (DO_DMA && J == 2)
+                                dma_piece(dbuf, std::integral_constant<int, 8 + I>{}, s, aoff, bs);
                             amma<CT, 4 * (8 * I + J), false>(fw[1][J], fa[H][I]);
                         }
                         __builtin_amdgcn_sched_barrier(0);
@@ -719,8 +759,10 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                     pinned_barrier();
                     if (H == 0) next_setup();
                     const int64_t o = a_koff(H);
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) dma_piece(H == 0 ? buf0 : buf1, i, H, o);
+                    const Bases bh = bases_of(H == 0 ? buf0 : buf1);
+                    static_for<16>([&](auto i_c) __attribute__((always_inline)) {
+                        dma_piece(H == 0 ? buf0 : buf1, i_c, H, o, bh);
+                    });
                 }
                 epi_fast(h_c, true, em0, en0, y_rsrc);
             };
@@ -778,12 +820,27 @@ bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32) {
     return (size_t)p.N * p.Kp < (1u << 31);
 }
 
+// VP3D_A4_GD=0 (measurement; read at every launch): one LDS base per DMA piece instead of
+// grouped pieces
+static bool a4_grouped() {
+    const char* e = getenv("VP3D_A4_GD");
+    return !(e && strcmp(e, "0") == 0);
+}
+
 hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream) {
     const dim3 grid(((p.M + GM - 1) / GM) * (p.N / GN));  // one tile per workgroup
-    if (out_f32)
-        hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 2>), grid, dim3(256), 0, stream, p);
-    else
-        hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 1>), grid, dim3(256), 0, stream, p);
+    const bool gd = a4_grouped();
+    if (out_f32) {
+        if (gd)
+            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 2, true>), grid, dim3(256), 0, stream, p);
+        else
+            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 2, false>), grid, dim3(256), 0, stream, p);
+    } else {
+        if (gd)
+            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 1, true>), grid, dim3(256), 0, stream, p);
+        else
+            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 1, false>), grid, dim3(256), 0, stream, p);
+    }
     return hipGetLastError();
 }
 
@@ -826,10 +883,18 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t
         return hipGetLastError();
     }
 #endif
-    if (compute == Act::BF16)
-        hipLaunchKernelGGL((conv_gemm_a4<__bf16, 0>), grid, dim3(256), 0, stream, p);
-    else
-        hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0>), grid, dim3(256), 0, stream, p);
+    const bool gd = a4_grouped();
+    if (compute == Act::BF16) {
+        if (gd)
+            hipLaunchKernelGGL((conv_gemm_a4<__bf16, 0, 0, true>), grid, dim3(256), 0, stream, p);
+        else
+            hipLaunchKernelGGL((conv_gemm_a4<__bf16, 0, 0, false>), grid, dim3(256), 0, stream, p);
+    } else {
+        if (gd)
+            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 0, true>), grid, dim3(256), 0, stream, p);
+        else
+            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 0, false>), grid, dim3(256), 0, stream, p);
+    }
     return hipGetLastError();
 }
 
