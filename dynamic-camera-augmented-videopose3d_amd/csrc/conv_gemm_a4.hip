@@ -645,10 +645,15 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                                        "+v"(x[3]), "+v"(y[3]));
                         float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
                         if (has_r) {
-                            const f16x8 rh = __builtin_bit_cast(f16x8, rres[I][jp][0]);
-                            const f16x8 rl = __builtin_bit_cast(f16x8, rres[I][jp][1]);
+                            // v + (rh + rl): the exact pair sums as mixed FMAs, then one f32 add each
+                            const u32x4 rh = rres[I][jp][0], rl = rres[I][jp][1];
 #pragma unroll
-                            for (int e = 0; e < 8; ++e) v[e] += (float)rh[e] + (float)rl[e];
+                            for (int e = 0; e < 4; ++e) {
+                                float t0, t1;
+                                gemm::x3_res_sum2(rh[e], rl[e], t0, t1);
+                                v[2 * e] += t0;
+                                v[2 * e + 1] += t1;
+                            }
                         }
                         const bool in = m < p.M;
                         if constexpr (X3 == 2) {
@@ -659,16 +664,17 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                             __builtin_amdgcn_raw_buffer_store_b128(
                                 __builtin_bit_cast(u32x4, f32x4{v[4], v[5], v[6], v[7]}), y_rsrc, yo + 16, 0, 0);
                         } else {
-                            f16x8 oh, ol;
+                            // hi = f16(v), lo = f16(v - hi) (v_fma_mixlo/mixhi: one rounding, as before)
+                            u32x4 oh, ol;
 #pragma unroll
-                            for (int e = 0; e < 8; ++e) {
-                                oh[e] = (f16)v[e];
-                                ol[e] = (f16)(v[e] - (float)oh[e]);
+                            for (int e = 0; e < 4; ++e) {
+                                oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
+                                ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                             }
                             const uint32_t yo =
                                 in ? (uint32_t)(((size_t)(m - m0) * p.ldy + 2 * nw + 64 * jp + c0) * 2) : 0xFFFFFF00u;
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, oh), y_rsrc, yo, 0, 0);
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ol), y_rsrc, yo + 64, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(oh, y_rsrc, yo, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(ol, y_rsrc, yo + 64, 0, 0);
                         }
                     }
                 });

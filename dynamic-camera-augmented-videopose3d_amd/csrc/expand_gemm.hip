@@ -309,20 +309,21 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                         v[d] = x;
                         v[d + 4] = y;
                     }
-                    f16x8 oh, ol;
+                    // hi = f16(v), lo = f16(v - hi) (v_fma_mixlo/mixhi: one rounding each)
+                    u32x4 oh, ol;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        oh[e] = (f16)v[e];
-                        ol[e] = (f16)(v[e] - (float)oh[e]);
+                    for (int e = 0; e < 4; ++e) {
+                        oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
+                        ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                     }
                     if (m < p.M) {
                         u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + 64 * jp + c0);
                         if constexpr (NT) {
-                            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, oh), dst);
-                            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, ol), dst + 4);
+                            __builtin_nontemporal_store(oh, dst);
+                            __builtin_nontemporal_store(ol, dst + 4);
                         } else {
-                            dst[0] = __builtin_bit_cast(u32x4, oh);
-                            dst[4] = __builtin_bit_cast(u32x4, ol);
+                            dst[0] = oh;
+                            dst[4] = ol;
                         }
                     }
                 }

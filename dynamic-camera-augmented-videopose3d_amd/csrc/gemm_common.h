@@ -454,6 +454,33 @@ __device__ __forceinline__ void epilogue_tp_rf(const ConvGemmParams& p, f32x4 (&
 // reference's res + relu(bn(conv)), TemporalModel.py:135,195).  Output: split (hi =
 // f16(v), lo = f16(v - hi)) or, OUT_F32, the f32 row for the exact f32 shrink GEMM.
 // 4 residual loads and 4 stores per row block: the waits count both.
+// Split-fp16 epilogue arithmetic on channel pairs as mixed-precision FMAs (the f16 sources widen
+// exactly, one rounding per result -- the same bits as the convert / f32 add / convert forms, in
+// fewer instructions):
+//   x3_res_sum2: a residual pair's hi + lo (f16 pairs, one dword each) as two exact f32 sums
+//   x3_split_lo2: the lo halves of an f32 pair whose hi halves (packed f16) are h: f16(x - hi),
+//                 written as one packed pair (v_fma_mixlo_f16 / v_fma_mixhi_f16)
+__device__ __forceinline__ void x3_res_sum2(uint32_t rh, uint32_t rl, float& t0, float& t1) {
+    asm("v_fma_mix_f32 %0, %2, 1.0, %3 op_sel_hi:[1,0,1]\n\t"
+        "v_fma_mix_f32 %1, %2, 1.0, %3 op_sel:[1,0,1] op_sel_hi:[1,0,1]"
+        : "=&v"(t0), "=v"(t1)
+        : "v"(rh), "v"(rl));
+}
+__device__ __forceinline__ uint32_t x3_split_lo2(uint32_t h, float x0, float x1) {
+    uint32_t r;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(r)
+        : "v"(h), "v"(x0), "v"(x1));
+    return r;
+}
+// f32 pair -> packed f16 pair (round to nearest even, one v_cvt_pk_f16_f32)
+__device__ __forceinline__ uint32_t x3_hi2(float x0, float x1) {
+    typedef float f2_ __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2_{x0, x1}, h2_));
+}
+
 template <bool OUT_F32, int HAS_R>
 __device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&acc)[8][4], int mw, int nw, int lane,
                                                const float* s_scale, const float* s_shift,
@@ -514,10 +541,15 @@ __device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&
                 v[d + 4] = y;
             }
             if (HAS_R) {
-                const f16x8 rh = __builtin_bit_cast(f16x8, res[i & 1][jp][0]);
-                const f16x8 rl = __builtin_bit_cast(f16x8, res[i & 1][jp][1]);
+                // v + (rh + rl): the exact pair sums as mixed FMAs, then one f32 add each
+                const u32x4 rh = res[i & 1][jp][0], rl = res[i & 1][jp][1];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] += (float)rh[e] + (float)rl[e];
+                for (int e = 0; e < 4; ++e) {
+                    float t0, t1;
+                    gemm::x3_res_sum2(rh[e], rl[e], t0, t1);
+                    v[2 * e] += t0;
+                    v[2 * e + 1] += t1;
+                }
             }
             const bool in = m < p.M;
             if constexpr (OUT_F32) {
@@ -527,16 +559,17 @@ __device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[4], v[5], v[6], v[7]}),
                                                        y_rsrc, yo + 16, 0, 0);
             } else {
-                f16x8 oh, ol;
+                // hi = f16(v), lo = f16(v - hi) (v_fma_mixlo/mixhi: one rounding, as before)
+                u32x4 oh, ol;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    oh[e] = (f16)v[e];
-                    ol[e] = (f16)(v[e] - (float)oh[e]);
+                for (int e = 0; e < 4; ++e) {
+                    oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
+                    ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                 }
                 const uint32_t yo = in ? (uint32_t)(((size_t)(m - m_base) * p.ldy + 2 * nw + 64 * jp + c0) * 2)
                                        : 0xFFFFFF00u;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, oh), y_rsrc, yo, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ol), y_rsrc, yo + 64, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(oh, y_rsrc, yo, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(ol, y_rsrc, yo + 64, 0, 0);
             }
         }
     }
