@@ -475,6 +475,10 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scale / shift stores
+        } else if constexpr (X3 != 0) {
+            // nothing to wait for: K-tiles 0 and 1 were issued before the previous epilogue's
+            // residual loads, which it waited for (vmcnt retires in issue order); only its last
+            // stores may still be in flight
         } else {
             // younger: K-tile 1 (16 pieces) and the previous epilogue's 32 stores (with a
             // residual: the H0 stores, K-tile 1, the H1 stores)
@@ -539,19 +543,27 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             using K1 = std::integral_constant<int, 1>;
             using K2 = std::integral_constant<int, 2>;
             // K-tile t in buffer `b` (the next one in `o`), A_hi in fa[H]
-            auto x3_ktile = [&](auto h_c, auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o)
+            // vm: the mid wait (K-tile 0 of a walked tile: 63 = none on vmcnt -- K-tile 1 was issued
+            // before the previous epilogue's residual loads, which that epilogue waited for, and
+            // vmcnt retires in issue order -- so that epilogue's last stores stay in flight)
+            auto x3_ktile = [&](auto h_c, auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o, int vm = 0)
                                 __attribute__((always_inline)) {
                 x3_phase(h_c, K0{}, zero_c, T_{}, F_{}, b, nullptr, 0);
-                mid(0);
+                if (vm == 63)
+                    __builtin_amdgcn_s_waitcnt(kLgkm0);
+                else
+                    __builtin_amdgcn_s_waitcnt(kVm0Lgkm0);
+                pinned_barrier();
                 x3_phase(h_c, K1{}, F_{}, rd_c, dma_c, o, b, t + 2);
                 x3_phase(h_c, K2{}, F_{}, rd_c, dma_c, o, b, t + 2);
             };
+            const int vm0 = first ? 0 : 63;
             if (nk > 2)
-                x3_ktile(C0{}, T_{}, T_{}, T_{}, 0, buf0, buf1);
+                x3_ktile(C0{}, T_{}, T_{}, T_{}, 0, buf0, buf1, vm0);
             else if (nk == 2)
-                x3_ktile(C0{}, T_{}, T_{}, F_{}, 0, buf0, buf1);
+                x3_ktile(C0{}, T_{}, T_{}, F_{}, 0, buf0, buf1, vm0);
             else
-                x3_ktile(C0{}, T_{}, F_{}, F_{}, 0, buf0, buf1);
+                x3_ktile(C0{}, T_{}, F_{}, F_{}, 0, buf0, buf1, vm0);
             int t = 1;
             for (; t + 3 < nk; t += 2) {
                 x3_ktile(C1{}, F_{}, T_{}, T_{}, t, buf1, buf0);
@@ -568,6 +580,15 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 x3_ktile(C1{}, F_{}, F_{}, F_{}, t, buf1, buf0);
             }
             asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+            // tile walk (the 1x1 + residual layers): every wave has passed the last K-tile's
+            // barrier after its last LDS reads, so both buffers take the next tile's K-tiles 0
+            // and 1 now, ahead of this tile's epilogue loads and stores (in flight under the
+            // next tile's first K-tiles); em0 / en0 keep this tile's origin
+            const int em0 = m0, en0 = n0;
+            if (has_next) {
+                setup(next);
+                stage_01();
+            }
             // split epilogue per 64 channels (the arithmetic of gemm::epilogue_tp_x3, so the same
             // bits): BN as v_pk_mul_f32 + v_pk_add_f32, ReLU as an integer max on the f32 bits,
             // v_permlane16_swap to 8 consecutive channels per lane, residual hi + lo added in f32,
@@ -575,23 +596,23 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             // residual of a whole half (8 row blocks x 2 x hi / lo, 128 VGPRs) is loaded up front
             // -- epilogue_tp_x3 loads it one row block ahead, a latency per row block
             constexpr int OB = X3 == 2 ? 4 : 2;  // output element bytes
-            const size_t y_rest = (size_t)(p.M - m0) * p.ldy * OB;
+            const size_t y_rest = (size_t)(p.M - em0) * p.ldy * OB;
             const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(
-                (const char*)p.Y + (size_t)m0 * p.ldy * OB, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+                (const char*)p.Y + (size_t)em0 * p.ldy * OB, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
             typedef float f32x2 __attribute__((ext_vector_type(2)));
             typedef int i32x2 __attribute__((ext_vector_type(2)));
             const bool has_r = p.R != nullptr;
-            const int rrow0 = has_r ? res_row(p, m0) : 0;
+            const int rrow0 = has_r ? res_row(p, em0) : 0;
             const __amdgpu_buffer_rsrc_t rx_rsrc =
                 make_rsrc(has_r ? (const f16*)p.R + (int64_t)rrow0 * p.ldr : (const f16*)p.A, 0x7FFFFFFFu);
             static_for<2>([&](auto hh_c) __attribute__((always_inline)) {
                 constexpr int HH = decltype(hh_c)::value;
-                const int nw = n0 + wc * 128 + 64 * HH;
+                const int nw = en0 + wc * 128 + 64 * HH;
                 u32x4 rres[8][2][2];  // [row block][jp][hi, lo]
                 if (has_r) {
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        int m = m0 + wr * 128 + 16 * i + (lane & 15);
+                        int m = em0 + wr * 128 + 16 * i + (lane & 15);
                         m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
                         const int off = ((res_row(p, m) - rrow0) * p.ldr + 2 * nw + c0) * 2;
 #pragma unroll
@@ -616,7 +637,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 }
                 static_for<8>([&](auto i_c) __attribute__((always_inline)) {
                     constexpr int I = decltype(i_c)::value;
-                    const int m = m0 + wr * 128 + 16 * I + (lane & 15);
+                    const int m = em0 + wr * 128 + 16 * I + (lane & 15);
                     float v4[4][4];  // [block j][element]: BN + ReLU, accumulator layout
                     static_for<4>([&](auto j_c) __attribute__((always_inline)) {
                         constexpr int J = decltype(j_c)::value;
@@ -658,7 +679,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                         const bool in = m < p.M;
                         if constexpr (X3 == 2) {
                             const uint32_t yo =
-                                in ? (uint32_t)(((size_t)(m - m0) * p.ldy + nw + 32 * jp + c0) * 4) : 0xFFFFFFE0u;
+                                in ? (uint32_t)(((size_t)(m - em0) * p.ldy + nw + 32 * jp + c0) * 4) : 0xFFFFFFE0u;
                             __builtin_amdgcn_raw_buffer_store_b128(
                                 __builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}), y_rsrc, yo, 0, 0);
                             __builtin_amdgcn_raw_buffer_store_b128(
@@ -672,14 +693,17 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                                 ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                             }
                             const uint32_t yo =
-                                in ? (uint32_t)(((size_t)(m - m0) * p.ldy + 2 * nw + 64 * jp + c0) * 2) : 0xFFFFFF00u;
+                                in ? (uint32_t)(((size_t)(m - em0) * p.ldy + 2 * nw + 64 * jp + c0) * 2) : 0xFFFFFF00u;
                             __builtin_amdgcn_raw_buffer_store_b128(oh, y_rsrc, yo, 0, 0);
                             __builtin_amdgcn_raw_buffer_store_b128(ol, y_rsrc, yo + 64, 0, 0);
                         }
                     }
                 });
             });
-            break;  // one tile per workgroup
+            if (!has_next) break;
+            tix = next;
+            first = false;
+            continue;
         } else {
         // K-tile 0 (phase A initialises the accumulators: C = 0), then the steady state (both
         // follow-up K-tiles exist: no branch inside a K-tile), then the last two K-tiles (with
@@ -833,8 +857,25 @@ static bool a4_grouped() {
     return !(e && strcmp(e, "0") == 0);
 }
 
+static int a4_cus() {
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        return n & ~7;
+    }();
+    return ncu;
+}
+
 hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream) {
-    const dim3 grid(((p.M + GM - 1) / GM) * (p.N / GN));  // one tile per workgroup
+    // the 1x1 + residual layers walk their tiles (one workgroup per CU, as launch_conv_gemm_a4);
+    // VP3D_A4_WALK 0: never, 2: every layer
+    const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+    const char* we = getenv("VP3D_A4_WALK");
+    const int walk_mode = we ? atoi(we) : 1;
+    const int ncu = a4_cus();
+    const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && ntiles > ncu;
+    const dim3 grid(walk ? ncu : ntiles);
     const bool gd = a4_grouped();
     if (out_f32) {
         if (gd)
