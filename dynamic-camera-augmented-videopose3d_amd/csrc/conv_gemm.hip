@@ -410,6 +410,69 @@ __global__ __launch_bounds__(256) void conv_gemm_narrow(ConvGemmParams p) {
     }
 }
 
+// Exact-f32 narrow layers (N <= 64: the shrink conv of the fp32 and split-fp16 paths,
+// TemporalModel.py:33 / :74; the sequence lifters' 51-wide output Linear): one wave per 16 rows
+// x 64 columns, operands straight from global memory (each lane: a 16-byte run of its row's K
+// and of 4 weight rows -- the weight rows stay in L1/L2 for every wave), the MFMA k order of
+// conv_gemm_f32 (v_mfma_f32_16x16x4_f32 s = 0..3 over the 16-deep step, lane group c holding
+// k = 16 kt + 4 c + s), so the same bits.  conv_gemm_f32 ran these on 128 x 128 tiles: 64 of
+// them at B = 8,192 windows, a 64-step K loop with a barrier per step on 64 CUs: 93 vs 54 us.
+// From 256 tiles of 128 rows on, the tile kernel stays ahead (B = 65,536: 0.164 vs 0.185 ms).
+__global__ __launch_bounds__(64) void conv_gemm_f32_narrow(ConvGemmParams p) {
+    const int lane = threadIdx.x;
+    const int c = lane >> 4, r = lane & 15;
+    const int m0 = blockIdx.x * 16;
+    const int m = m0 + r;
+    const bool mv = m < p.M;
+    const float* const arow = (const float*)p.A + (int64_t)(mv ? src_row(p, m) : 0) * p.lda + 4 * c;
+    const float* wrow[4];
+    bool nv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = 16 * j + r;
+        nv[j] = n < p.N;
+        wrow[j] = (const float*)p.W + (int64_t)(nv[j] ? n : 0) * p.Kp + 4 * c;
+    }
+    f32x4 acc[1][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nk = p.K / 16;
+    f32x4 a = mv ? *(const f32x4*)arow : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = nv[j] ? *(const f32x4*)wrow[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+        // the next step's operands in flight under this step's 16 MFMAs
+        const bool more = kt + 1 < nk;
+        f32x4 an = f32x4{0.f, 0.f, 0.f, 0.f}, wn[4] = {an, an, an, an};
+        if (more) {
+            if (mv) an = *(const f32x4*)(arow + 16 * (kt + 1));
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (nv[j]) wn[j] = *(const f32x4*)(wrow[j] + 16 * (kt + 1));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], w[j][s], acc[0][j], 0, 0, 0);
+        a = an;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = wn[j];
+    }
+    epilogue_scalar<float, 1>(p, acc, m0, 0, lane);
+}
+
+// VP3D_F32_NARROW=0 (measurement; read at every launch): the tile kernel instead
+bool getenv_flag_off(const char* name) {
+    const char* e = getenv(name);
+    return !(e && e[0] == '0' && e[1] == 0);
+}
+
+bool f32_narrow_eligible(const ConvGemmParams& p) {
+    return p.N <= 64 && p.M < 256 * BM && !p.R && p.Ktap == p.K && p.K % 16 == 0 && p.K <= p.Kp && p.lda % 4 == 0 &&
+           p.Kp % 4 == 0 && aligned(p.A, 16) && aligned(p.W, 16) && getenv_flag_off("VP3D_F32_NARROW");
+}
+
 bool narrow_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
     // only while the 128-row tiles would leave CUs idle (< 256 tiles): B = 8192 windows
     // 0.036 -> 0.018 ms; at 65,536 rows the tile kernel stays ahead (0.048 vs 0.086 ms)
@@ -432,6 +495,10 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
                       (!p.R || ((p.ldr % 8 == 0) && aligned(p.R, 16))) && oes > 0;
     if (compute == Act::F32) {
         if (a_type != Act::F32 || out_type != Act::F32) return hipErrorInvalidValue;
+        if (f32_narrow_eligible(p)) {
+            hipLaunchKernelGGL(conv_gemm_f32_narrow, dim3((p.M + 15) / 16), dim3(64), 0, stream, p);
+            return hipGetLastError();
+        }
         if ((p.Ktap % kF32Bk == 0) && (p.lda % 4 == 0) && aligned(p.A, 16))
             return launch_f32<A_VEC>(p, vepi, grid, stream);
         if (contiguous && (p.lda % 2 == 0) && (p.K % 2 == 0) && aligned(p.A, 8))

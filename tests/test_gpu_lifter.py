@@ -263,3 +263,19 @@ def test_shape_asserts_and_short_input():
         m(torch.zeros(20, 16, 2, device="cuda"))
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 5, 17, 2, device="cuda"))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
+def test_f32_narrow_shrink_bit_identical(dtype, monkeypatch):
+    """The exact-f32 narrow GEMM that runs the shrink (N = 51) keeps conv_gemm_f32's MFMA k
+    order: the same bits as the tile kernel (VP3D_F32_NARROW=0), on a ragged batch (the narrow
+    kernel takes M < 32,768 rows)."""
+    model, _ = make_model(True, seed=0)
+    model = model.cuda()
+    model.set_compute_dtype(dtype)
+    x = torch.from_numpy(synth.normalized_windows(11, "narrow", 1000, 243)).cuda()
+    with torch.no_grad():
+        y_new = model(x).cpu().numpy()
+        monkeypatch.setenv("VP3D_F32_NARROW", "0")
+        y_old = model(x).cpu().numpy()
+    assert np.array_equal(y_new, y_old)

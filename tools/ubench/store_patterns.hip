@@ -23,7 +23,15 @@ __global__ __launch_bounds__(256) void k_contig(u32x4* y, long n16) {
 }
 
 // one workgroup = 256 rows, 4 waves x 64 rows, 16 chunks of 64 channels
-template <int MODE>
+template <typename T>
+__device__ __forceinline__ void st(T* p, T v, bool nt) {
+    if (nt)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+template <int MODE, bool NT = false>
 __global__ __launch_bounds__(256) void k_chunk(char* y, int M) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const long m_wave = (long)blockIdx.x * 256 + wid * 64;
@@ -33,7 +41,7 @@ __global__ __launch_bounds__(256) void k_chunk(char* y, int M) {
             // 8 lanes per row (8 x 16 B = 128 B), 8 rows per instruction, 8 instructions
             for (int q = 0; q < 8; ++q) {
                 const long m = m_wave + q * 8 + (lane >> 3);
-                if (m < M) *(u32x4*)(y + m * 2048 + col + (lane & 7) * 16) = u32x4{1u, 2u, 3u, (unsigned)ch};
+                if (m < M) st((u32x4*)(y + m * 2048 + col + (lane & 7) * 16), u32x4{1u, 2u, 3u, (unsigned)ch}, NT);
             }
         } else if (MODE == 2) {
             // MFMA-transposed layout: row l&15, 4 lane groups x 8 B, j = 0..3 blocks of 32 B
@@ -48,7 +56,7 @@ __global__ __launch_bounds__(256) void k_chunk(char* y, int M) {
                 for (int jp = 0; jp < 2; ++jp) {
                     const long m = m_wave + rb * 16 + (lane & 15);
                     const int seg = ((lane >> 4) & 1) * 2 + (lane >> 5);  // 0..3 x 16 B
-                    if (m < M) *(u32x4*)(y + m * 2048 + col + jp * 64 + seg * 16) = u32x4{1u, 2u, 3u, (unsigned)ch};
+                    if (m < M) st((u32x4*)(y + m * 2048 + col + jp * 64 + seg * 16), u32x4{1u, 2u, 3u, (unsigned)ch}, NT);
                 }
         }
         __builtin_amdgcn_s_barrier();
@@ -73,8 +81,9 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[] = {"contiguous", "chunk128_16B", "chunk128_8B", "chunk128_16B_p", "rowfull_16B"};
-    for (int mode = 0; mode < 5; ++mode) {
+    const char* names[] = {"contiguous", "chunk128_16B", "chunk128_8B", "chunk128_16B_p", "rowfull_16B",
+                           "chunk128_16B nt", "chunk128_16B_p nt"};
+    for (int mode = 0; mode < 7; ++mode) {
         float best = 1e30f;
         for (int rep = 0; rep < 6; ++rep) {
             hipEventRecord(a, 0);
@@ -84,6 +93,8 @@ int main(int argc, char** argv) {
                 case 2: hipLaunchKernelGGL(k_chunk<2>, dim3((M + 255) / 256), dim3(256), 0, 0, y, M); break;
                 case 3: hipLaunchKernelGGL(k_chunk<3>, dim3((M + 255) / 256), dim3(256), 0, 0, y, M); break;
                 case 4: hipLaunchKernelGGL(k_rowfull, dim3((M + 63) / 64), dim3(256), 0, 0, y, M); break;
+                case 5: hipLaunchKernelGGL((k_chunk<1, true>), dim3((M + 255) / 256), dim3(256), 0, 0, y, M); break;
+                case 6: hipLaunchKernelGGL((k_chunk<3, true>), dim3((M + 255) / 256), dim3(256), 0, 0, y, M); break;
             }
             hipEventRecord(b, 0);
             hipEventSynchronize(b);
