@@ -516,8 +516,7 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
         return hipGetLastError();
     }
     const int gm = gemm_8p_mode();
-    if ((gm == 5 || gm == 1) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
-        conv_gemm_a4_eligible(p, a_type, out_type, compute))
+    if ((gm == 5 || gm == 1) && conv_gemm_a4_eligible(p, a_type, out_type, compute) && conv_gemm_a4_fills(p))
         return launch_conv_gemm_a4(p, compute, stream);
     if ((gm == 3 || (gm == 1 && p.dil == 1)) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_q64_eligible(p, a_type, out_type, compute))

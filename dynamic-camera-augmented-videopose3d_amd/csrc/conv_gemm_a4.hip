@@ -131,7 +131,7 @@ __device__ __forceinline__ float aread() {
 __device__ unsigned long long* g_a4_trace;
 #endif
 
-template <typename CT, int ABL, int X3 = 0, bool GD = true>
+template <typename CT, int ABL, int X3 = 0, bool GD = true, bool SPLIT = false>
 __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     // the accumulator file is this kernel's own from here on (see the header)
     asm volatile("" ::: A4_ALL_AGPRS);
@@ -157,13 +157,23 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     const int ntn = p.N / GN;
     const int ntm = (p.M + GM - 1) / GM;
     const int ntiles = ntm * ntn;
-    const int nk = p.Kp / GK;  // >= 1
+    const int nk_all = p.Kp / GK;  // >= 1
+    // Work units: tile u < sk_full whole; with a split plan (ConvGemmParams::sk_*) the sk_left
+    // tiles after them as S units each -- unit full + v: tile full + v % L, K range q = S - 1 -
+    // v / L (helpers first, the owner q = 0 dispatched last: the owners wait for their helpers,
+    // which never wait).  Per unit: kb / nk (first K-tile, K-tiles), role, the tile's slot.
+    const int S = SPLIT ? p.sk_split : 1;  // SPLIT launches only (no split code otherwise)
+    const int sk_full = S > 1 ? p.sk_full : ntiles;
+    const int nunits = S > 1 ? sk_full + S * p.sk_left : ntiles;
+    constexpr int kWhole = 0, kOwner = 1, kHelper = 2;
+    int kb = 0, nk = nk_all, role = kWhole, sidx = 0, sq = 0;
     // 1x1 convs (residual): the tile's residual rows land in LDS by LDS-DMA during the last
     // two K-tiles, into the operand buffers those no longer need -- part h (the channel half
     // h of both wave columns: 256 rows x 2 x 128 B = 64 KiB) in phase B of tile nk - 2 + h,
     // in the DMA slots; rows at 128-byte pitch with the operands' chunk swizzle -- so the
     // epilogue reads them from LDS instead of waiting on global loads row block by row block
-    const bool lres = X3 == 0 && p.R != nullptr && nk >= 3;
+    const bool lres_layer = X3 == 0 && p.R != nullptr && nk_all >= 3;
+    bool lres = lres_layer;  // per unit: helpers run no epilogue
 #ifdef VP3D_ABLATION
     unsigned long long* const trc = (ABL & 4) && g_a4_trace ? g_a4_trace + (size_t)blockIdx.x * 10 : nullptr;
     unsigned long long mid_cyc = 0;
@@ -197,7 +207,21 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     int m0 = 0, n0 = 0;
     uint32_t va[8], vw[8], vr[8];
     __amdgpu_buffer_rsrc_t a_rsrc, w_rsrc, r_rsrc;
-    auto setup = [&](int tix) __attribute__((always_inline)) {
+    auto setup = [&](int unit) __attribute__((always_inline)) {
+        int tix = unit;
+        kb = 0;
+        nk = nk_all;
+        role = kWhole;
+        if (S > 1 && unit >= sk_full) {
+            const int v = unit - sk_full;
+            sidx = v % p.sk_left;
+            sq = S - 1 - v / p.sk_left;
+            tix = sk_full + sidx;
+            kb = sq * (nk_all / S);
+            nk = nk_all / S;
+            role = sq == 0 ? kOwner : kHelper;
+        }
+        lres = lres_layer && role != kHelper && nk >= 3;
         const int wg = xcd_remap(tix, ntiles);
         const int tile_m = wg / ntn;
         const int tile_n = wg - tile_m * ntn;
@@ -261,7 +285,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     };
     // k offset of K-tile s inside a row: tap * dil rows + channel base (wave-uniform)
     auto a_koff = [&](int s) __attribute__((always_inline)) -> int64_t {
-        const int k0 = s * GK;
+        const int k0 = (kb + s) * GK;
         const int tap = k0 / p.Ktap;
         return (int64_t)tap * p.dil * p.lda + (k0 - tap * p.Ktap);
     };
@@ -273,7 +297,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                                                      (uint32_t)aoff * (uint32_t)sizeof(CT), GD ? (i & 3) * 1024 : 0, 0);
         else
             __builtin_amdgcn_raw_ptr_buffer_load_lds(w_rsrc, (lds_ptr_t)ldsp, 16, vw[i - 8],
-                                                     (uint32_t)(s * GK * (int)sizeof(CT)), GD ? (i & 3) * 1024 : 0, 0);
+                                                     (uint32_t)((kb + s) * GK * (int)sizeof(CT)), GD ? (i & 3) * 1024 : 0, 0);
     };
     char* const buf0 = smem;
     char* const buf1 = smem + GBUF;
@@ -392,11 +416,53 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     // a residual part in registers (accumulator layout), so its buffer can take one of the
     // next tile's first two K-tiles before that half's stores
     u32x2 resr[8][4];
+    int enk = nk;  // the K-tiles of the unit whose epilogue runs (the next unit's setup may be done)
     auto res_addr = [&](int h, int i, int j) __attribute__((always_inline)) -> const u32x2* {
-        return (const u32x2*)(smem + ((nk - 2 + h) & 1) * GBUF + wc * 256 * 128 + wr * 128 * 128 + (lane & 15) * 128 +
+        return (const u32x2*)(smem + ((enk - 2 + h) & 1) * GBUF + wc * 256 * 128 + wr * 128 * 128 + (lane & 15) * 128 +
                               (grp & 1) * 8 + i * 2048 + (((2 * j + (grp >> 1)) ^ fsw) << 4));
     };
-    auto epi_fast = [&](auto h_c, bool with_res, int em0, int en0, __amdgpu_buffer_rsrc_t y_rsrc) __attribute__((always_inline)) {
+    // ---- split-K partial sums: a helper unit stores its 256 accumulators per lane (64 x 16 B,
+    // [wave][block / 4][lane] in its 256 KiB slot: whole 1 KiB runs per instruction), releases
+    // them at agent scope (the owner may sit on another XCD) and counts itself in the tile's
+    // flag; the owner waits for S - 1 (bounded: 1 s, never expected), acquires, and adds the
+    // helpers' values to its own, in unit order, as it reads its accumulators ----
+    auto part_ptr = [&](int si, int q) __attribute__((always_inline)) -> float* {
+        return p.sk_part + (size_t)(si * (S - 1) + (q - 1)) * 65536 + (size_t)wid * 16384 + lane * 4;
+    };
+    auto helper_store = [&](int si, int q) __attribute__((always_inline)) {
+        float* const base = part_ptr(si, q);
+        static_for<64>([&](auto r_c) __attribute__((always_inline)) {
+            constexpr int R4 = decltype(r_c)::value;
+            *(f32x4*)(base + R4 * 256) = f32x4{aread<4 * R4>(), aread<4 * R4 + 1>(), aread<4 * R4 + 2>(), aread<4 * R4 + 3>()};
+        });
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        pinned_barrier();
+        if (tid == 0) __hip_atomic_fetch_add(p.sk_flag + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto owner_wait = [&](int si) __attribute__((always_inline)) {
+        if (tid == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(p.sk_flag + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) break;
+            }
+        }
+        pinned_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    };
+    // v (the accumulators of block R as two pairs) += the helpers' values of that block
+    auto owner_add = [&](auto r_c, int si, f32x2 (&v)[2]) __attribute__((always_inline)) {
+        constexpr int R = decltype(r_c)::value;
+        for (int q = 1; q < S; ++q) {
+            const f32x4 pr = *(const f32x4*)(part_ptr(si, q) + (R / 4) * 256);
+            v[0] = v[0] + f32x2{pr[0], pr[1]};
+            v[1] = v[1] + f32x2{pr[2], pr[3]};
+        }
+    };
+    auto owner_done = [&](int si) __attribute__((always_inline)) {
+        if (tid == 0) __hip_atomic_store(p.sk_flag + si, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto epi_fast = [&](auto h_c, bool with_res, int em0, int en0, __amdgpu_buffer_rsrc_t y_rsrc, int own_si) __attribute__((always_inline)) {
         constexpr int H = decltype(h_c)::value;
         const int nw = en0 + wc * 128 + 64 * H;
         f32x2 sc[4][2], sh[4][2];
@@ -418,6 +484,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 constexpr int J = decltype(j_c)::value;
                 constexpr int R = 4 * (8 * I + 4 * H + J);
                 f32x2 v[2] = {f32x2{aread<R>(), aread<R + 1>()}, f32x2{aread<R + 2>(), aread<R + 3>()}};
+                if (own_si >= 0) owner_add(std::integral_constant<int, R>{}, own_si, v);
                 ct4 r4;
                 if (with_res) r4 = __builtin_bit_cast(ct4, resr[I][J]);
 #pragma unroll
@@ -450,7 +517,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     };
     using H0 = std::integral_constant<int, 0>;
     using H1 = std::integral_constant<int, 1>;
-    const int res0 = lres ? 0 : -1, res1 = lres ? 1 : -1;
+    int res0 = -1, res1 = -1;  // per unit (below)
 
     // ---- the tiles of this workgroup: blockIdx.x, + gridDim.x, ... (a grid of one
     // workgroup per CU walks them; with one tile per workgroup the loop runs once).  The
@@ -461,6 +528,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     setup(tix);
     stage_01();
     bool first = true;
+    bool prev_lres = false;  // the previous unit's epilogue took residual parts (its store order)
     for (;;) {
         // the per-lane constants go through an empty asm every tile: otherwise the compiler
         // hoists every address derived from them out of the tile loop and keeps them live
@@ -468,7 +536,9 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         launder_lane_consts(prow, lc, fsw, fo0, fo1, a_base, w_base, grp, c0);
         launder_params(p);
         const int next = tix + (int)gridDim.x;
-        const bool has_next = next < ntiles;
+        const bool has_next = next < nunits;
+        res0 = lres ? 0 : -1;
+        res1 = lres ? 1 : -1;
         if (first) {
             if (nk > 1)
                 asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // K-tile 0 landed (younger: K-tile 1)
@@ -585,10 +655,19 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             // and 1 now, ahead of this tile's epilogue loads and stores (in flight under the
             // next tile's first K-tiles); em0 / en0 keep this tile's origin
             const int em0 = m0, en0 = n0;
+            const int erole = role, esidx = sidx, esq = sq;
             if (has_next) {
                 setup(next);
                 stage_01();
             }
+            if (erole == kHelper) {
+                helper_store(esidx, esq);
+                if (!has_next) break;
+                tix = next;
+                first = false;
+                continue;
+            }
+            if (erole == kOwner) owner_wait(esidx);
             // split epilogue per 64 channels (the arithmetic of gemm::epilogue_tp_x3, so the same
             // bits): BN as v_pk_mul_f32 + v_pk_add_f32, ReLU as an integer max on the f32 bits,
             // v_permlane16_swap to 8 consecutive channels per lane, residual hi + lo added in f32,
@@ -643,6 +722,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                         constexpr int J = decltype(j_c)::value;
                         constexpr int R = 4 * (8 * I + 4 * HH + J);
                         f32x2 v[2] = {f32x2{aread<R>(), aread<R + 1>()}, f32x2{aread<R + 2>(), aread<R + 3>()}};
+                        if (erole == kOwner) owner_add(std::integral_constant<int, R>{}, esidx, v);
 #pragma unroll
                         for (int q = 0; q < 2; ++q) {
                             f32x2 x = v[q] * sc[J][q];
@@ -700,6 +780,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                     }
                 });
             });
+            if (erole == kOwner) owner_done(esidx);
             if (!has_next) break;
             tix = next;
             first = false;
@@ -710,7 +791,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         // nk >= 3 always the tail's last two calls)
         // mid(0) of a later tile: K-tile 1 landed, younger stores may stay in flight (32; with
         // a residual the H1 stores only, 16)
-        const int vm0 = first ? 0 : lres ? 16 : 32;
+        const int vm0 = first ? 0 : prev_lres ? 16 : 32;
         if (nk > 2)
             ktile(T_{}, T_{}, T_{}, 0, buf0, buf1, -1, vm0);
         else if (nk == 2)
@@ -721,6 +802,9 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         if (first) stamp(1);
 #endif
         const int em0 = m0, en0 = n0;
+        enk = nk;
+        const int erole = role, esidx = sidx, esq = sq;
+        const bool elres = lres;
         // the next tile's addressing once this tile's last operand DMA has been issued
         auto next_setup = [&]() __attribute__((always_inline)) {
             if (has_next) setup(next);
@@ -762,12 +846,18 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         if (trc && tid == 0) trc[9] = mid_cyc;
 #endif
 
+        if (erole == kHelper) {  // split-K helper: no epilogue (never followed by another unit)
+            helper_store(esidx, esq);
+            break;
+        }
+        if (erole == kOwner) owner_wait(esidx);
+        const int own_si = erole == kOwner ? esidx : -1;
         // the output resource starts at the tile's first row (outputs past 2^31 bytes: the
         // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
         const size_t y_rest = (size_t)(p.M - em0) * p.ldy * sizeof(CT);
         const __amdgpu_buffer_rsrc_t y_rsrc =
             make_rsrc((const CT*)p.Y + (size_t)em0 * p.ldy, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
-        if (lres) {
+        if (elres) {
             // residual part h into registers once landed (every wave's pieces: after the
             // barrier), then its buffer takes the next tile's K-tile h (nk even: part h sits in
             // buffer h) before the half-h stores: issue order part 0, part 1, K-tile 0, H0
@@ -794,14 +884,16 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                         dma_piece(H == 0 ? buf0 : buf1, i_c, H, o, bh);
                     });
                 }
-                epi_fast(h_c, true, em0, en0, y_rsrc);
+                epi_fast(h_c, true, em0, en0, y_rsrc, own_si);
             };
             part(H0{});
             part(H1{});
         } else {  // no residual (the eligibility check leaves no residual with nk < 3)
-            epi_fast(H0{}, false, em0, en0, y_rsrc);
-            epi_fast(H1{}, false, em0, en0, y_rsrc);
+            epi_fast(H0{}, false, em0, en0, y_rsrc, own_si);
+            epi_fast(H1{}, false, em0, en0, y_rsrc, own_si);
         }
+        if (erole == kOwner) owner_done(esidx);
+        prev_lres = elres;
         if (!has_next) break;
         tix = next;
         first = false;
@@ -845,16 +937,10 @@ bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32) {
     if ((reinterpret_cast<uintptr_t>(p.A) & 15) || (reinterpret_cast<uintptr_t>(p.Y) & 15) ||
         (reinterpret_cast<uintptr_t>(p.W) & 15) || (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
         return false;
-    // enough tiles to fill the CUs (as the 16-bit dispatch: >= 384 tiles of 256 x 256)
-    if ((int64_t)((p.M + GM - 1) / GM) * (p.N / GN) < 384) return false;
+    // enough tiles to fill the CUs (as the 16-bit dispatch: >= 384 tiles of 256 x 256), or a
+    // split plan that does
+    if (!conv_gemm_a4_fills(p)) return false;
     return (size_t)p.N * p.Kp < (1u << 31);
-}
-
-// VP3D_A4_GD=0 (measurement; read at every launch): one LDS base per DMA piece instead of
-// grouped pieces
-static bool a4_grouped() {
-    const char* e = getenv("VP3D_A4_GD");
-    return !(e && strcmp(e, "0") == 0);
 }
 
 static int a4_cus() {
@@ -867,52 +953,97 @@ static int a4_cus() {
     return ncu;
 }
 
-hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream) {
+// Split-K plan of a launch's partial last round: L = the tiles past the last whole round of the
+// chip's CUs, each split into S = CUs / L units (<= 4) of an equal whole number (even, >= 4) of
+// K-tiles, so the last round is S x L <= CUs units of 1 / S the work.  Config 4 at N = 8 (8,192
+// windows per GPU) leaves L = 128 in every block (block 4 has 128 tiles in all) -> S = 2.  Taken
+// only for long K (>= 64 K-tiles: the split-fp16 k3 convs) over few rounds (< 8): the helper's
+// 256 KiB of partial sums, the owner's wait and adds and the split variant's extra scalar
+// registers (spilled to VGPR lanes) cost about an epilogue, and every unit of the launch runs
+// the split variant.  Measured at B = 8,192 (profiles/r04q_split_k_ab.txt): f16x3 block-2 /
+// 3 / 4 k3 0.977 / 0.361 / 0.154 vs 0.994 / 0.387 / 0.187 ms whole-tile; block-1 k3 (13.5
+// rounds) 2.707 vs 2.692; every 1x1 (16-32 K-tiles) and every bf16 layer slower (bf16 block-3
+// 1x1 0.100 vs 0.061 ms).  Needs the handle's workspace (sk_part); VP3D_A4_SPLIT=0
+// (measurement; read at every launch) turns it off, 2 takes it wherever it fits.  Returns the
+// plan in q.sk_* (sk_split 0: none).
+static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk) {
+    q.sk_split = q.sk_full = q.sk_left = 0;
+    const char* e = getenv("VP3D_A4_SPLIT");
+    const int mode = e ? atoi(e) : 1;
+    if (mode == 0 || !q.sk_part || !q.sk_flag) return;
+    const int ncu = a4_cus();
+    if (ncu <= 0 || ncu > 256) return;  // the workspace holds one round of 256 slots
+    if (mode == 1 && (nk < 64 || ntiles >= 8 * ncu)) return;
+    const int L = ntiles % ncu;
+    if (L == 0) return;
+    int S = ncu / L;
+    S = S > 4 ? 4 : S;
+    while (S >= 2 && (nk % S != 0 || nk / S < 4 || (nk / S) % 2 != 0)) --S;
+    if (S < 2) return;
+    q.sk_full = ntiles - L;
+    q.sk_split = S;
+    q.sk_left = L;
+}
+
+// the tile count from which a4 is the kernel of a 16-bit layer (fewer: q64 / the 128 x 128
+// kernel), unless a split plan fills the chip (config 4's block 4 at N = 8: 128 tiles)
+bool conv_gemm_a4_fills(const ConvGemmParams& p) {
+    const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+    if (ntiles >= 384) return true;
+    ConvGemmParams q = p;
+    a4_split_plan(q, ntiles, p.Kp / GK);
+    return q.sk_split > 1;
+}
+
+template <typename CT, int X3>
+static void a4_launch(const ConvGemmParams& p, dim3 grid, bool split, hipStream_t stream) {
+    if (split)
+        hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, true>), grid, dim3(256), 0, stream, p);
+    else
+        hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), grid, dim3(256), 0, stream, p);
+}
+
+hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p_in, bool out_f32, hipStream_t stream) {
     // the 1x1 + residual layers walk their tiles (one workgroup per CU, as launch_conv_gemm_a4);
     // VP3D_A4_WALK 0: never, 2: every layer
-    const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+    const int ntiles = ((p_in.M + GM - 1) / GM) * (p_in.N / GN);
+    ConvGemmParams p = p_in;
+    a4_split_plan(p, ntiles, p.Kp / GK);
+    const bool split = p.sk_split > 1;
+    const int nunits = split ? p.sk_full + p.sk_split * p.sk_left : ntiles;
     const char* we = getenv("VP3D_A4_WALK");
     const int walk_mode = we ? atoi(we) : 1;
     const int ncu = a4_cus();
-    const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && ntiles > ncu;
-    const dim3 grid(walk ? ncu : ntiles);
-    const bool gd = a4_grouped();
-    if (out_f32) {
-        if (gd)
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 2, true>), grid, dim3(256), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 2, false>), grid, dim3(256), 0, stream, p);
-    } else {
-        if (gd)
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 1, true>), grid, dim3(256), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 1, false>), grid, dim3(256), 0, stream, p);
-    }
+    const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && nunits > ncu;
+    const dim3 grid(walk ? ncu : nunits);
+    if (out_f32)
+        a4_launch<_Float16, 2>(p, grid, split, stream);
+    else
+        a4_launch<_Float16, 1>(p, grid, split, stream);
     return hipGetLastError();
 }
 
-hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream) {
-    const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+hipError_t launch_conv_gemm_a4(const ConvGemmParams& p_in, Act compute, hipStream_t stream) {
+    const int ntiles = ((p_in.M + GM - 1) / GM) * (p_in.N / GN);
     // Tile walk (one workgroup per CU; a multiple of 8 keeps each workgroup on one XCD's tile
     // range under round-robin placement) for the 1x1 + residual convs: the next tile's first
     // two K-tiles then land under this tile's epilogue and no workgroup launch gap separates
     // the tiles (B = 65,536, same box: block-1 1x1 3.69-3.70 vs 3.78-3.86 ms, blocks 2-4
     // -4..-8 %); the k3 convs keep one tile per workgroup (walked: the same or up to 2 %
     // slower).  With a residual the walk needs nk even (residual part h sits in the buffer
-    // of the next tile's K-tile h).  VP3D_A4_WALK (measurement; read at every launch, so a
-    // test can flip it): 0 never, 2 every layer.
+    // of the next tile's K-tile h; the split plan keeps every unit's nk even).  VP3D_A4_WALK
+    // (measurement; read at every launch, so a test can flip it): 0 never, 2 every layer.
     const char* we = getenv("VP3D_A4_WALK");
     const int walk_mode = we ? atoi(we) : 1;
-    static const int ncu = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 0;
-        return n & ~7;
-    }();
-    const int nk = p.Kp / GK;
-    const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && nk >= 3 && ntiles > ncu &&
+    const int ncu = a4_cus();
+    const int nk = p_in.Kp / GK;
+    ConvGemmParams p = p_in;
+    a4_split_plan(p, ntiles, nk);
+    const bool split = p.sk_split > 1;
+    const int nunits = split ? p.sk_full + p.sk_split * p.sk_left : ntiles;
+    const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && nk >= 3 && nunits > ncu &&
                       (!p.R || nk % 2 == 0);
-    const dim3 grid(walk ? ncu : ntiles);
+    const dim3 grid(walk ? ncu : nunits);
 #ifdef VP3D_ABLATION
     // measurement builds only (tools/ubench/gemm_check): VP3D_ABL=1 no loop DMA, 2 no loop
     // fragment reads, 3 neither (wrong results, timing only), 4 stamps
@@ -921,27 +1052,21 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t
         return e ? atoi(e) : 0;
     }();
     if (compute == Act::BF16 && abl >= 1) {
+        p.sk_split = 0;
+        const dim3 g(walk ? ncu : ntiles);
         switch (abl) {
-            case 1: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 1>), grid, dim3(256), 0, stream, p); break;
-            case 2: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 2>), grid, dim3(256), 0, stream, p); break;
-            case 3: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 3>), grid, dim3(256), 0, stream, p); break;
-            default: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 4>), grid, dim3(256), 0, stream, p); break;
+            case 1: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 1>), g, dim3(256), 0, stream, p); break;
+            case 2: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 2>), g, dim3(256), 0, stream, p); break;
+            case 3: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 3>), g, dim3(256), 0, stream, p); break;
+            default: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 4>), g, dim3(256), 0, stream, p); break;
         }
         return hipGetLastError();
     }
 #endif
-    const bool gd = a4_grouped();
-    if (compute == Act::BF16) {
-        if (gd)
-            hipLaunchKernelGGL((conv_gemm_a4<__bf16, 0, 0, true>), grid, dim3(256), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_a4<__bf16, 0, 0, false>), grid, dim3(256), 0, stream, p);
-    } else {
-        if (gd)
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 0, true>), grid, dim3(256), 0, stream, p);
-        else
-            hipLaunchKernelGGL((conv_gemm_a4<_Float16, 0, 0, false>), grid, dim3(256), 0, stream, p);
-    }
+    if (compute == Act::BF16)
+        a4_launch<__bf16, 0>(p, grid, split, stream);
+    else
+        a4_launch<_Float16, 0>(p, grid, split, stream);
     return hipGetLastError();
 }
 

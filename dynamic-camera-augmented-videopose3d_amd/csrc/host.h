@@ -110,6 +110,9 @@ struct vp3d_handle {
     // window-gather scratch of vp3d_forward_windows when the fused expand path does not apply
     float* gather_ws = nullptr;
     size_t gather_bytes = 0;
+    // split-K workspace of conv_gemm_a4 (ConvGemmParams::sk_part / sk_flag; flags zeroed once,
+    // each owner unit resets its own)
+    void* sk_ws = nullptr;
     // profiling
     bool profiling = false;
     uint64_t prof_mask = ~0ull;  // layers timed while profiling (bit i = layer i)

@@ -33,7 +33,20 @@ struct ConvGemmParams {
     int R_T, R_stride, R_off, ldr;
     int ldy;
     int relu;  // 0: none, 1: ReLU, 2: LeakyReLU(0.01) (the 16-bit 256x256 kernels: 0/1 only)
+    // conv_gemm_a4 only: split-K of a launch's partial last round of 256 x 256 tiles.  The host
+    // provides the workspace (sk_part: 256 KiB per helper unit, at most one round of them;
+    // sk_flag: one zeroed int per tile of that round); the launcher fills the plan (sk_split 0 =
+    // whole tiles only): tiles [0, sk_full) whole, each of the sk_left tiles after them as
+    // sk_split units of nk / sk_split K-tiles -- the helper units store their f32 accumulators,
+    // the owner unit (the first K range) adds them, in unit order, before its epilogue.
+    float* sk_part;
+    int* sk_flag;
+    int sk_full, sk_split, sk_left;
 };
+
+// bytes of the split-K workspace a handle provides (ConvGemmParams::sk_part, then the flags)
+constexpr size_t kSplitPartBytes = (size_t)256 * 256 * 1024;  // one round of 256 KiB slots
+constexpr size_t kSplitFlagBytes = 4096;
 
 enum class Act { F32 = 0, BF16 = 1, F16 = 2 };
 
@@ -56,6 +69,8 @@ hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_
 // One wave per SIMD, 128 x 128 wave tiles, accumulators in named AGPRs (conv_gemm_a4.hip);
 // same contract as q64.
 bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
+// >= 384 tiles of 256 x 256, or fewer that a split-K plan spreads over every CU
+bool conv_gemm_a4_fills(const ConvGemmParams& p);
 hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream);
 // Split-fp16 mode of conv_gemm_a4 (the q64 contract above, N % 256 == 0, >= 384 tiles); the same
 // bits as conv_gemm_q64_x3.

@@ -357,6 +357,10 @@ int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
     // three rotating activation buffers + (16-bit path) the packed expand-conv rows
     const size_t need = 3 * rows * h->cfg.channels * esize(dtype) +
                         (dtype == VP3D_DTYPE_F32 ? 0 : rows * h->layers[0].Kp * (dtype == VP3D_DTYPE_F16X3 ? 4 : 2));
+    if (!h->sk_ws) {
+        HIP_TRY(hipMalloc(&h->sk_ws, vp3d::kSplitPartBytes + vp3d::kSplitFlagBytes));
+        HIP_TRY(hipMemset((char*)h->sk_ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitFlagBytes));
+    }
     if (need <= h->ws_bytes) return VP3D_OK;
     if (h->ws) HIP_TRY(hipFree(h->ws));
     h->ws = nullptr;
@@ -433,6 +437,7 @@ int vp3d_destroy(vp3d_handle* h) {
     free_layers(h);
     if (h->ws) hipFree(h->ws);
     if (h->gather_ws) hipFree(h->gather_ws);
+    if (h->sk_ws) hipFree(h->sk_ws);
     for (auto& e : h->pending) {
         hipEventDestroy(e.a);
         hipEventDestroy(e.b);
@@ -532,6 +537,8 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         p.lda = L.cin;
         p.relu = L.relu ? 1 : 0;
         p.ldy = L.cout;
+        p.sk_part = (float*)h->sk_ws;
+        p.sk_flag = (int*)((char*)h->sk_ws + kSplitPartBytes);
         p.W = dtype == VP3D_DTYPE_F32 ? (const void*)L.w32
                                       : (dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh);
         int out_buf = -1;

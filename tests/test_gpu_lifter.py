@@ -141,6 +141,8 @@ def test_gemm_a4_bit_identical_to_q64(dtype, walk, monkeypatch):
     fp16 mode (three f16 MFMAs per product, q64's order) against q64's, then the fp32 gates."""
     if walk is not None:
         monkeypatch.setenv("VP3D_A4_WALK", walk)
+    # whole tiles only: a split-K last round (below) sums those tiles in two chains
+    monkeypatch.setenv("VP3D_A4_SPLIT", "0")
     model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
     x = synth.normalized_windows(1, "x4100_243", 4100, 243)
     model.cuda().set_compute_dtype(dtype)
@@ -164,6 +166,7 @@ def test_dilated_seq_a4_bit_identical_to_q64(dtype, monkeypatch):
     """VP3D_GEMM=a4 puts the dilated k3 convs of a long sequence (taps d rows apart: the tile's
     k offset steps d rows at every tap) on conv_gemm_a4; q64 sums in the same order.  40,000
     frames: every block layer has >= 384 tiles of 256 x 256 (both kernels' threshold)."""
+    monkeypatch.setenv("VP3D_A4_SPLIT", "0")  # whole tiles only (a split-K last round sums in two chains)
     model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
     x = synth.normalized_windows(1, "x1_40000", 1, 40000)
     model.cuda().set_compute_dtype(dtype)
@@ -279,3 +282,34 @@ def test_f32_narrow_shrink_bit_identical(dtype, monkeypatch):
         monkeypatch.setenv("VP3D_F32_NARROW", "0")
         y_old = model(x).cpu().numpy()
     assert np.array_equal(y_new, y_old)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f16x3"])
+def test_a4_split_k_last_round(dtype, monkeypatch):
+    """Config 4's per-GPU share at N = 8 (8,192 windows): every block leaves 128 tiles past the
+    last whole round of 256 CUs, which conv_gemm_a4 can run as 2 half-K units each (the owner
+    adds the helper's f32 partial sums before its epilogue; block 4's 128 tiles in all) --
+    VP3D_A4_SPLIT=2: on every layer it fits, walked 1x1 layers and bf16 included.  Against
+    the whole-tile run (VP3D_A4_SPLIT=0): f16x3 within 1e-6 m (only the partial sums' rounding
+    differs), bf16 within its coordinate gate; both against the oracle on the first and last
+    64 windows under their dtype's gates."""
+    monkeypatch.setenv("VP3D_A4_SPLIT", "2")  # every layer it fits (default: the f16x3 k3 convs)
+    model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
+    B = 8192
+    x = synth.normalized_windows(5, "x8192_243", B, 243)
+    model.cuda().set_compute_dtype(dtype)
+    xd = torch.from_numpy(x).cuda()
+    with torch.no_grad():
+        y = model(xd).cpu().numpy()
+        y2 = model(xd).cpu().numpy()
+        monkeypatch.setenv("VP3D_A4_SPLIT", "0")
+        y_whole = model(xd).cpu().numpy()
+    assert np.isfinite(y).all()
+    assert np.array_equal(y, y2)  # deterministic: the owner adds the partials in unit order
+    d = float(np.abs(y - y_whole).max())
+    print(f"{dtype}: split vs whole-tile max|d| {d:.3e} m")
+    assert d <= (1e-6 if dtype == "f16x3" else H16_TOL[dtype][0]), d
+    sel = np.r_[0:64, B - 64:B]
+    ref = lifter_forward(sd, x[sel], [3, 3, 3, 3, 3], causal=False, strided=True, dense=False).numpy()
+    gt = synth.gt_poses(3, "gt", 128, 17).reshape(ref.shape)
+    _check(y[sel], ref, gt, dtype)
