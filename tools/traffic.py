@@ -15,6 +15,7 @@ are KiB; on gfx950 FETCH_SIZE tallies each 128-byte read request as 64 bytes, so
 the read side is doubled.  WRITE_SIZE is exact for 16-byte-per-lane stores.
 """
 import argparse
+import sys
 import csv
 import glob
 import json
@@ -44,10 +45,12 @@ def forwards(rows, B):
     expand_grids = {((B * 81 + 255) // 256) * 256, ((B * 81 + 127) // 128) * 256}
     # other expand forms (f16x3: two workgroups per CU): the largest expand grid in the trace
     expand_grids.add(max((g for n, g, _ in rows.values() if "expand_gemm" in n), default=0))
+    # the fp32 path: the expand conv on the 128 x 128 f32 tile kernel (1024 channels)
+    f32_expand = ((B * 81 + 127) // 128) * 8 * 256
     i = 0
     while i < len(ids):
         name, grid, _ = rows[ids[i]]
-        start = ("expand_gemm" in name and grid in expand_grids)
+        start = ("expand_gemm" in name and grid in expand_grids) or ("conv_gemm_f32" in name and grid == f32_expand)
         if not start:
             i += 1
             continue
