@@ -267,7 +267,10 @@ __device__ __forceinline__ void trace_mark(const StreamPipeParams& p, int wg, in
 
 }  // namespace
 
-template <typename WT, int KS>
+// SERVE: the serve form (p.serve; the resident one-frame-in-flight launch) as its own
+// instantiation, so the graph form carries none of its end protocol (with it inline the
+// pipelined step measured 2.82 vs 2.38 us, same box: profiles/r04w_stream_serve_split_ab.txt)
+template <typename WT, int KS, bool SERVE>
 __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipeParams p) {
     constexpr int CWK = kPipeCwK, CWP = kPipeCwP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -278,8 +281,8 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     const int C = p.C, nb = p.nb, nl = p.nl, Q = p.queue;
     // serve form: downstream waits also watch the end word and may last the expand role's
     // idle budget (frames arrive at the host's pace)
-    const unsigned* const endw = p.serve ? p.end_frame : nullptr;
-    const unsigned long long limit = p.serve ? p.fault.spin_ticks + p.idle_ticks : p.fault.spin_ticks;
+    const unsigned* const endw = SERVE ? p.end_frame : nullptr;
+    const unsigned long long limit = SERVE ? p.fault.spin_ticks + p.idle_ticks : p.fault.spin_ticks;
     const int nE = 2 * nb + 1;
     // per-role parameters selected with compile-time indices (a runtime index into the
     // by-value kernel argument would copy it to scratch)
@@ -382,7 +385,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         for (int s = 0;; ++s) {
             const int t = t0 + s;
             float fv = 0.f;  // element tid (< cin0) of frame t
-            if (!p.serve) {
+            if (!SERVE) {
                 if (s >= p.steps) break;
                 if (tid < cin0) fv = p.frames[(int64_t)(t & (Q - 1)) * cin0 + tid];
             } else {
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 nh1 = v;
             }
             __syncthreads();
-            if (p.serve && end_flag) {
+            if (SERVE && end_flag) {
                 // frame t was never posted: the history stays; a rolled-back frame t - 1 leaves
                 // no trace (history as before it, its output granules untagged)
                 if (rollback_flag) {
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             hp2 = nh2;
             // serve: commit frame t (speculatively: its outputs go out before the answer,
             // checked at the next frame)
-            if (p.serve && tid == 0)
+            if (SERVE && tid == 0)
                 claim_old = __hip_atomic_fetch_max(p.end_claim, (unsigned)t + 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
             trace_mark(p, wg, s, 0, tid);
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         const float sc = lead ? scl[cr - c_lo] : 0.f, sh = lead ? scl[kPipeMaxCh + cr - c_lo] : 0.f;
         Pref pf;
         pref_issue(pf, edge(role - 1, t0), C, tid);
-        for (int s = 0; p.serve || s < p.steps; ++s) {
+        for (int s = 0; SERVE || s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
             if (!pref_finish(pf, edge(role - 1, t), C, (unsigned)t + 1u, xv, &abort_flag, p.fault, tid, pause,
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             if (abort_flag) return;
             if (end_flag) break;
             trace_mark(p, wg, s, 0, tid);
-            if (p.serve || s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
+            if (SERVE || s + 1 < p.steps) pref_issue(pf, edge(role - 1, t + 1), C, tid);  // in flight during this frame
             f2 xl[KS / 2];
             load_x<KS>(xl, xv, lane);
             float vp[CWK];
@@ -581,7 +584,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         Pref pf, pr;
         pref_issue(pr, edge(role - 2, t0, c_lo), nres, tid);
         pref_issue(pf, edge(role - 1, t0), C, tid);
-        for (int s = 0; p.serve || s < p.steps; ++s) {
+        for (int s = 0; SERVE || s < p.steps; ++s) {
             const int t = t0 + s;
             float* xv = xbuf + (s & 1) * C;
             float* rv = rbuf + (s & 1) * kPipeMaxCh;
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             if (abort_flag) return;
             if (end_flag) break;
             trace_mark(p, wg, s, 0, tid);
-            if (p.serve || s + 1 < p.steps) {  // the next frame's loads are in flight during this one
+            if (SERVE || s + 1 < p.steps) {  // the next frame's loads are in flight during this one
                 pref_issue(pr, edge(role - 2, t + 1, c_lo), nres, tid);
                 pref_issue(pf, edge(role - 1, t + 1), C, tid);
             }
@@ -609,7 +612,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                     y = y > 0.f ? y : 0.f;
                     y += rv[cr - c_lo];
                     publish(out_at(role, t, cr), (unsigned)t + 1u, y);
-                } else if (p.serve) {
+                } else if (SERVE) {
                     // host-mapped pose ring: the granule's tag tells the host it is there
                     const unsigned long long g = ((unsigned long long)((unsigned)t + 1u) << 32) | __float_as_uint(y);
                     __hip_atomic_store(p.pose_gran + (int64_t)(t & (Q - 1)) * Nout + cr, g, __ATOMIC_RELAXED,
@@ -633,7 +636,7 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             if (l == nl) active = p.cu0[l];
         if (prev == (unsigned)active - 1u) {
             *p.arrivals = 0u;
-            const int t_end = p.serve ? (int)__hip_atomic_load(p.end_frame, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+            const int t_end = SERVE ? (int)__hip_atomic_load(p.end_frame, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                       : t0 + p.steps;
             __hip_atomic_store(p.frames_seen, t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -646,7 +649,13 @@ int stream_pipe_lds_bytes(int C, int cin0, int max_ring) {
 
 hipError_t launch_stream_pipe(const StreamPipeParams& p, Act wtype, int lds_bytes, hipStream_t s) {
     const dim3 grid(p.cu0[p.nl]);
-#define VP3D_PIPE(WT, KS) hipLaunchKernelGGL((stream_pipe_kernel<WT, KS>), grid, dim3(kThreads), lds_bytes, s, p)
+#define VP3D_PIPE(WT, KS)                                                                                  \
+    do {                                                                                                   \
+        if (p.serve)                                                                                       \
+            hipLaunchKernelGGL((stream_pipe_kernel<WT, KS, true>), grid, dim3(kThreads), lds_bytes, s, p);  \
+        else                                                                                               \
+            hipLaunchKernelGGL((stream_pipe_kernel<WT, KS, false>), grid, dim3(kThreads), lds_bytes, s, p); \
+    } while (0)
     const int KS = p.C / 64;
     if (wtype == Act::F16 && KS == 16) VP3D_PIPE(_Float16, 16);
     else if (wtype == Act::F16 && KS == 4) VP3D_PIPE(_Float16, 4);
@@ -664,13 +673,27 @@ bool stream_pipe_channels_ok(int C) { return C == 1024 || C == 256; }
 namespace vp3d {
 
 hipError_t stream_pipe_prepare(Act wtype, int C, int lds_bytes) {
-    const void* f = nullptr;
-    if (wtype == Act::F16 && C == 1024) f = (const void*)stream_pipe_kernel<_Float16, 16>;
-    else if (wtype == Act::F16 && C == 256) f = (const void*)stream_pipe_kernel<_Float16, 4>;
-    else if (wtype == Act::BF16 && C == 1024) f = (const void*)stream_pipe_kernel<__bf16, 16>;
-    else if (wtype == Act::BF16 && C == 256) f = (const void*)stream_pipe_kernel<__bf16, 4>;
-    else return hipErrorInvalidValue;
-    return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    const void* f[2] = {nullptr, nullptr};
+    if (wtype == Act::F16 && C == 1024) {
+        f[0] = (const void*)stream_pipe_kernel<_Float16, 16, false>;
+        f[1] = (const void*)stream_pipe_kernel<_Float16, 16, true>;
+    } else if (wtype == Act::F16 && C == 256) {
+        f[0] = (const void*)stream_pipe_kernel<_Float16, 4, false>;
+        f[1] = (const void*)stream_pipe_kernel<_Float16, 4, true>;
+    } else if (wtype == Act::BF16 && C == 1024) {
+        f[0] = (const void*)stream_pipe_kernel<__bf16, 16, false>;
+        f[1] = (const void*)stream_pipe_kernel<__bf16, 16, true>;
+    } else if (wtype == Act::BF16 && C == 256) {
+        f[0] = (const void*)stream_pipe_kernel<__bf16, 4, false>;
+        f[1] = (const void*)stream_pipe_kernel<__bf16, 4, true>;
+    } else {
+        return hipErrorInvalidValue;
+    }
+    for (const void* g : f) {
+        const hipError_t e = hipFuncSetAttribute(g, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace vp3d
