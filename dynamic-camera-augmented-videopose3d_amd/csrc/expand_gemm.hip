@@ -96,7 +96,18 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
-    const int m_wave = blockIdx.x * kRows + wid * kRowsW;
+    // workgroups [0, sk_full): a whole row block each; after them each remaining row block is
+    // sk_split workgroups of an equal channel-chunk range (the launcher's fill of the partial
+    // last round, dispatched last)
+    const int nchunks = p.N / kExpChunkN;
+    int rblk = blockIdx.x, ch_lo = 0, ch_hi = nchunks;
+    if (rblk >= p.sk_full) {
+        const int u = rblk - p.sk_full, part = u % p.sk_split;
+        rblk = p.sk_full + u / p.sk_split;
+        ch_lo = part * nchunks / p.sk_split;
+        ch_hi = (part + 1) * nchunks / p.sk_split;
+    }
+    const int m_wave = rblk * kRows + wid * kRowsW;
     u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * 128);
     float* const s_scale = (float*)(smem + RING * kChunk);
     float* const s_shift = s_scale + kExpMaxN;
@@ -112,15 +123,14 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     const int dc = ((lane & 3) - 2 * ((dr >> 2) & 3)) & 3;
     const CT* const wsrc = (const CT*)p.W + (int64_t)dr * p.Kp + dc * 8;
     auto stage_w = [&](int chunk) {
-        char* dst = smem + (chunk % RING) * kChunk + wid * 1024;
+        char* dst = smem + ((chunk - ch_lo) % RING) * kChunk + wid * 1024;
         const CT* src = wsrc + (int64_t)chunk * kExpChunkN * p.Kp;
 #pragma unroll
         for (int q = 0; q < NKW; ++q)
             __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + q * 32), (lds_ptr_t)(dst + q * kExpSlab), 16, 0, 0);
     };
-    const int nchunks = p.N / kExpChunkN;
-    stage_w(0);
-    if (RING == 3 && nchunks > 1) stage_w(1);
+    stage_w(ch_lo);
+    if (RING == 3 && ch_lo + 1 < ch_hi) stage_w(ch_lo + 1);
 
     // ---- A fragments: row (l & 15) of each 16-row block, k = 32*ks + 8*(l>>4) .. +7;
     // k = K, K + 1 are the bias columns (1.0), k > K + 1 zero ----
@@ -245,11 +255,11 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     // ReLU on the packed 16-bit results: max with +0 (bits 0); no ReLU: max with the
     // smallest int16, a no-op
     const short2v floor2 = p.relu ? short2v{0, 0} : short2v{-32768, -32768};
-    for (int ch = 0; ch < nchunks; ++ch) {
+    for (int ch = ch_lo; ch < ch_hi; ++ch) {
         // chunk ch + 2 goes to the slot chunk ch - 1 used: every wave passed the barrier
         // that ended chunk ch - 1 after its last fragment read there
-        if (ch + RING - 1 < nchunks) stage_w(ch + RING - 1);
-        const char* wb = smem + (ch % RING) * kChunk;
+        if (ch + RING - 1 < ch_hi) stage_w(ch + RING - 1);
+        const char* wb = smem + ((ch - ch_lo) % RING) * kChunk;
         f32x4 acc[RB][4];
         if constexpr (X3) {
 #pragma unroll
@@ -329,10 +339,10 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                 }
             }
             asm volatile("" ::: "memory");
-            if (ch + 1 < nchunks) {
+            if (ch + 1 < ch_hi) {
                 if (m_wave + kRowsW > p.M)
                     exp_vm<0>();
-                else if (RING == 3 && ch + 2 < nchunks)
+                else if (RING == 3 && ch + 2 < ch_hi)
                     exp_vm<NKW + 4 * RB>();
                 else
                     exp_vm<4 * RB>();  // this chunk's stores: RB row blocks x 2 channel halves x (hi, lo)
@@ -395,10 +405,10 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
         // the next chunk's weights: younger are chunk ch + 2's DMA (if issued) and this
         // chunk's 2 * RB stores.  A wave with rows past M may skip store instructions
         // (all lanes masked): fewer younger operations, so it drains everything instead.
-        if (ch + 1 < nchunks && abl != 4) {
+        if (ch + 1 < ch_hi && abl != 4) {
             if (m_wave + kRowsW > p.M || abl == 2)
                 exp_vm<0>();
-            else if (RING == 3 && ch + 2 < nchunks)
+            else if (RING == 3 && ch + 2 < ch_hi)
                 exp_vm<NKS + 2 * RB>();
             else
                 exp_vm<2 * RB>();
@@ -407,9 +417,41 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     }
 }
 
+// resident workgroup slots per launch: two per CU (__launch_bounds__(256, 2); the
+// NKS = 5 variants hold one, and then the split round below is two rounds of half the size)
+static int exp_slots() {
+    static const int n = [] {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        return 2 * ncu;
+    }();
+    return n;
+}
+
+// One workgroup per row block, except in a partial last round: with L < slots row blocks
+// past the last whole round (or in all, for small M), each is split into S = min(slots / L, 8) workgroups of 16 / S
+// channel chunks (dispatched last), so that round takes 1 / S of a round's time
+// (B = 8,192: the f16x3 expand is 10.1 rounds of 512 row blocks, the bf16 one 5.06).
+// Measured there: expand 0.85 vs 0.87 ms (f16x3), 0.295 vs 0.305 ms (bf16), +0.3-0.6 % per
+// step -- the memory-bound tail was already short, its few row blocks running with the
+// whole chip's bandwidth (profiles/r04x_expand_split_round_ab.txt).
+// VP3D_EXPAND_SPLIT=0 (measurement) keeps whole row blocks.
 template <typename CT, int RB, bool GATHER, bool NT, int RING = 3, bool X3 = false>
-hipError_t launch_rb_nt(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStream_t s) {
-    const dim3 grid((p.M + 64 * RB - 1) / (64 * RB));
+hipError_t launch_rb_nt(const ConvGemmParams& p_in, const GatherSrc& g, int nks, hipStream_t s) {
+    ConvGemmParams p = p_in;
+    const int nrb = (p.M + 64 * RB - 1) / (64 * RB);
+    const int slots = exp_slots();
+    const int left = slots > 0 ? nrb % slots : 0;
+    int S = left > 0 ? slots / left : 1;
+    S = S > 8 ? 8 : S;
+    const int nchunks = p.N / kExpChunkN;
+    while (S > 1 && nchunks % S) --S;
+    const char* off = getenv("VP3D_EXPAND_SPLIT");  // read at every launch (the A/B tests flip it)
+    if (off && off[0] == '0') S = 1;
+    p.sk_full = S > 1 ? nrb - left : nrb;
+    p.sk_split = S;
+    const dim3 grid(p.sk_full + (S > 1 ? left * S : 0));
     switch (nks) {
         case 1: hipLaunchKernelGGL((expand_gemm_h16<CT, 1, RB, GATHER, NT, RING, X3>), grid, dim3(256), 0, s, p, g); break;
         case 2: hipLaunchKernelGGL((expand_gemm_h16<CT, 2, RB, GATHER, NT, RING, X3>), grid, dim3(256), 0, s, p, g); break;

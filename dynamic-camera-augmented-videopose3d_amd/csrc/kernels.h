@@ -39,6 +39,8 @@ struct ConvGemmParams {
     // whole tiles only): tiles [0, sk_full) whole, each of the sk_left tiles after them as
     // sk_split units of nk / sk_split K-tiles -- the helper units store their f32 accumulators,
     // the owner unit (the first K range) adds them, in unit order, before its epilogue.
+    // expand_gemm reuses sk_full / sk_split for its N split of the partial last round: row
+    // blocks [0, sk_full) whole, each later one as sk_split workgroups of a channel range.
     float* sk_part;
     int* sk_flag;
     int sk_full, sk_split, sk_left;

@@ -313,3 +313,21 @@ def test_a4_split_k_last_round(dtype, monkeypatch):
     ref = lifter_forward(sd, x[sel], [3, 3, 3, 3, 3], causal=False, strided=True, dense=False).numpy()
     gt = synth.gt_poses(3, "gt", 128, 17).reshape(ref.shape)
     _check(y[sel], ref, gt, dtype)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "f16x3"])
+@pytest.mark.parametrize("B", [8192, 300])
+def test_expand_split_round_bit_identical(dtype, B, monkeypatch):
+    """expand_gemm runs a partial last round of row blocks (or all of them, for small M) as
+    channel-range workgroups (B = 8,192: 32 / 64 row blocks past 5 / 10 whole rounds of 512
+    slots -> 8 workgroups each; B = 300: under one round).  Each output element keeps its own
+    K order, so the stack's output is bit-identical to whole row blocks (VP3D_EXPAND_SPLIT=0)."""
+    model, _ = make_model(True, (3, 3, 3, 3, 3), False, 1024)
+    x = torch.from_numpy(synth.normalized_windows(9, f"xs{B}", B, 243)).cuda()
+    model.cuda().set_compute_dtype(dtype)
+    with torch.no_grad():
+        y = model(x).cpu().numpy()
+        monkeypatch.setenv("VP3D_EXPAND_SPLIT", "0")
+        y_whole = model(x).cpu().numpy()
+    assert np.isfinite(y).all()
+    assert np.array_equal(y, y_whole)
