@@ -529,6 +529,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     stage_01();
     bool first = true;
     bool prev_lres = false;  // the previous unit's epilogue took residual parts (its store order)
+    bool x3_prev_res = false;  // X3: the previous unit's epilogue loaded residual rows after its DMA
     for (;;) {
         // the per-lane constants go through an empty asm every tile: otherwise the compiler
         // hoists every address derived from them out of the tile loop and keeps them live
@@ -546,9 +547,12 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scale / shift stores
         } else if constexpr (X3 != 0) {
-            // nothing to wait for: K-tiles 0 and 1 were issued before the previous epilogue's
-            // residual loads, which it waited for (vmcnt retires in issue order); only its last
-            // stores may still be in flight
+            // with a residual nothing to wait for: K-tiles 0 and 1 were issued before the
+            // previous epilogue's residual loads, which it waited for (vmcnt retires in issue
+            // order); only its last stores may still be in flight.  Without one (a walked layer
+            // with no residual: VP3D_A4_WALK=2; a helper unit's release fence drained anyway)
+            // they may not have landed: drain.
+            if (!x3_prev_res) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             // younger: K-tile 1 (16 pieces) and the previous epilogue's 32 stores (with a
             // residual: the H0 stores, K-tile 1, the H1 stores)
@@ -662,6 +666,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             }
             if (erole == kHelper) {
                 helper_store(esidx, esq);
+                x3_prev_res = false;
                 if (!has_next) break;
                 tix = next;
                 first = false;
@@ -680,7 +685,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 (const char*)p.Y + (size_t)em0 * p.ldy * OB, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
             typedef float f32x2 __attribute__((ext_vector_type(2)));
             typedef int i32x2 __attribute__((ext_vector_type(2)));
-            const bool has_r = p.R != nullptr;
+            const bool has_r = p.R != nullptr;  // (helpers left above)
             const int rrow0 = has_r ? res_row(p, em0) : 0;
             const __amdgpu_buffer_rsrc_t rx_rsrc =
                 make_rsrc(has_r ? (const f16*)p.R + (int64_t)rrow0 * p.ldr : (const f16*)p.A, 0x7FFFFFFFu);
@@ -781,6 +786,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 });
             });
             if (erole == kOwner) owner_done(esidx);
+            x3_prev_res = has_r;
             if (!has_next) break;
             tix = next;
             first = false;

@@ -104,6 +104,27 @@ def _run(cmd):
     return r.stdout
 
 
+LLVM_BIN = os.environ.get("VP3D_LLVM_BIN", "/opt/rocm/lib/llvm/bin")
+# kernels that own the accumulator file through inline asm (named AGPRs, no clobbers per
+# MFMA): the compiler must never place a value of its own in an AGPR there
+AGPR_OWNERS = ("conv_gemm_a4.hip",)
+
+
+def agpr_writes(obj: str) -> int:
+    """v_accvgpr_write instructions in the gfx950 code object of a compiled translation unit.
+    In conv_gemm_a4 every AGPR holds an accumulator the MFMAs write through inline asm, so a
+    v_accvgpr_write there is the register allocator spilling a VGPR into the accumulator file
+    (it happens once the kernel needs more than 256 VGPRs) -- silently wrong results."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fatbin"), os.path.join(d, "dev.co")
+        _run([os.path.join(LLVM_BIN, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", obj, os.path.join(d, "x.o")])
+        _run([os.path.join(LLVM_BIN, "clang-offload-bundler"), "--type=o", f"--input={fb}",
+              f"--targets=hipv4-amdgcn-amd-amdhsa--{ARCH}", f"--output={co}", "--unbundle"])
+        dis = _run([os.path.join(LLVM_BIN, "llvm-objdump"), "-d", co])
+    return dis.count("v_accvgpr_write")
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -> str:
     """Compile every stale translation unit (in parallel: hipcc is single-threaded
     per file) and link libvp3d.so."""
@@ -138,6 +159,12 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None) -
                 if verbose and out.strip():
                     print(out)
         for _, obj, tu in todo:
+            if os.path.basename(obj)[:-2] in AGPR_OWNERS:
+                n = agpr_writes(obj)
+                if n:
+                    os.remove(obj)
+                    raise RuntimeError(f"build failed: {os.path.basename(obj)} spills {n} values into the "
+                                       "accumulator registers (v_accvgpr_write): cut VGPR pressure")
             with open(obj + ".sha", "w") as f:
                 f.write(tu + "\n")
     if force or todo or embedded_hash() != want:

@@ -71,3 +71,15 @@ def test_null_arguments():
     assert lib.vp3d_forward(None, None, 1, 1, None, 0, None) == N.VP3D_ERR_ARG
     assert lib.vp3d_receptive_field(None) == -1
     assert lib.vp3d_destroy(None) == N.VP3D_OK
+
+
+def test_no_values_spilled_into_accumulator_registers():
+    """conv_gemm_a4 owns all 256 AGPRs through inline-asm MFMAs (no per-instruction clobbers),
+    so any v_accvgpr_write in its code object is the allocator spilling a VGPR there -- a
+    silently corrupted accumulator.  build() refuses such an object; this checks the one the
+    library was linked from."""
+    from vp3d_amd import build as B
+    obj = os.path.join(B.BUILD_DIR, "conv_gemm_a4.hip.o")
+    if not os.path.exists(obj):
+        pytest.skip("library objects not built here")
+    assert B.agpr_writes(obj) == 0

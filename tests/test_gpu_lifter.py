@@ -130,7 +130,7 @@ def test_gemm_kernel_override(gemm, opt1f, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype,walk", [("bf16", None), ("fp16", None), ("bf16", "0"), ("bf16", "2"),
-                                        ("f16x3", None)])
+                                        ("f16x3", None), ("f16x3", "2")])
 def test_gemm_a4_bit_identical_to_q64(dtype, walk, monkeypatch):
     """The one-wave-per-SIMD AGPR kernel (conv_gemm_a4.hip, the default for the strided k3
     and 1x1 + residual convs with >= 384 tiles) sums every output in q64's K order (two
