@@ -303,7 +303,6 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
             }
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
-                const int m = m_wave + rb * 16 + (lane & 15);
 #pragma unroll
                 for (int jp = 0; jp < 2; ++jp) {
                     float v[8];
@@ -326,15 +325,54 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                         oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
                         ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                     }
-                    if (m < p.M) {
-                        u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + 64 * jp + c0);
-                        if constexpr (NT) {
-                            __builtin_nontemporal_store(oh, dst);
-                            __builtin_nontemporal_store(ol, dst + 4);
-                        } else {
-                            dst[0] = oh;
-                            dst[4] = ol;
+                    const int r16 = lane & 15;
+                    if constexpr (NKS > 4) {
+                        // (the camera-concat shape, one workgroup per CU: the two 64-byte halves
+                        // of 16 lines per instruction measured faster there, 7.54 vs 7.74 ms)
+                        const int m = m_wave + rb * 16 + r16;
+                        if (m < p.M) {
+                            u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + 64 * jp + c0);
+                            if constexpr (NT) {
+                                __builtin_nontemporal_store(oh, dst);
+                                __builtin_nontemporal_store(ol, dst + 4);
+                            } else {
+                                dst[0] = oh;
+                                dst[4] = ol;
+                            }
                         }
+                        continue;
+                    }
+                    // whole 128-byte lines per store instruction: the line of row r holds its 32
+                    // hi then 32 lo channels; lanes of rows 8-15 of the 16 trade with rows 0-7 (DPP
+                    // row_ror:8) so instruction A writes rows 0-7 (hi from lanes 0-7, lo from lanes
+                    // 8-15) and instruction B rows 8-15 -- instead of two 64-byte halves of 16 lines
+                    // (config 4, B = 65,536: expand 5.24-5.26 vs 5.64-5.72 ms, same box;
+                    // profiles/r04final_x3_expand_whole_lines_ab.txt)
+                    const bool top = r16 < 8;
+                    u32x4 va, vb;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const uint32_t ol8 = (uint32_t)__builtin_amdgcn_mov_dpp((int)ol[e], 0x128, 0xF, 0xF, false);
+                        const uint32_t oh8 = (uint32_t)__builtin_amdgcn_mov_dpp((int)oh[e], 0x128, 0xF, 0xF, false);
+                        va[e] = top ? oh[e] : ol8;
+                        vb[e] = top ? oh8 : ol[e];
+                    }
+                    const int mrow = m_wave + rb * 16;
+                    const int ra = top ? r16 : r16 - 8, rbw = top ? r16 + 8 : r16;
+                    const int half = top ? 0 : 32;  // lo 64 bytes further
+                    if (mrow + ra < p.M) {
+                        u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)(mrow + ra) * p.ldy + 2 * n0 + 64 * jp + c0 + half);
+                        if constexpr (NT)
+                            __builtin_nontemporal_store(va, dst);
+                        else
+                            *dst = va;
+                    }
+                    if (mrow + rbw < p.M) {
+                        u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)(mrow + rbw) * p.ldy + 2 * n0 + 64 * jp + c0 + half);
+                        if constexpr (NT)
+                            __builtin_nontemporal_store(vb, dst);
+                        else
+                            *dst = vb;
                     }
                 }
             }
