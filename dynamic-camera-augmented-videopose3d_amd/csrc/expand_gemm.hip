@@ -88,10 +88,14 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     constexpr int kRows = kRowsW * kExpWaves;
     constexpr int NKW = X3 ? 2 * NKS : NKS;  // weight slabs per chunk
     constexpr int kChunk = NKW * kExpSlab;
+    // X3 with NKS = 5 (the camera concat): the 2 x 40 KB weight ring alone fills half the LDS, so
+    // the scale / shift rows are read from global memory per chunk (ahead of its weight DMA)
+    // instead of an 8 KB LDS copy -- two workgroups per CU instead of one
+    constexpr bool kSsLds = !(X3 && NKS > 4);
     // ring of weight chunks, then (16-bit) per-wave output staging: kRowsW rows x 128 B,
     // 16-byte unit c of row r at c ^ (r & 7); X3: scale, shift (N floats each) instead
     __shared__ __attribute__((aligned(16))) char smem[RING * kChunk +
-                                                      (X3 ? 2 * kExpMaxN * 4 : kExpWaves * kRowsW * 128)];
+                                                      (X3 ? (kSsLds ? 2 * kExpMaxN * 4 : 0) : kExpWaves * kRowsW * 128)];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * 128);
     float* const s_scale = (float*)(smem + RING * kChunk);
     float* const s_shift = s_scale + kExpMaxN;
-    if constexpr (X3) {
+    if constexpr (X3 && kSsLds) {
         for (int i = tid; i < p.N; i += 256) {
             s_scale[i] = p.scale[i];
             s_shift[i] = p.shift[i];
@@ -258,6 +262,15 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     for (int ch = ch_lo; ch < ch_hi; ++ch) {
         // chunk ch + 2 goes to the slot chunk ch - 1 used: every wave passed the barrier
         // that ended chunk ch - 1 after its last fragment read there
+        f32x4 gs4[kSsLds ? 1 : 4], gh4[kSsLds ? 1 : 4];  // !kSsLds: this chunk's scale / shift
+        if constexpr (!kSsLds) {
+            const int gc = ch * kExpChunkN + 4 * (lane >> 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                gs4[j] = *(const f32x4*)(p.scale + gc + 16 * j);
+                gh4[j] = *(const f32x4*)(p.shift + gc + 16 * j);
+            }
+        }
         if (ch + RING - 1 < ch_hi) stage_w(ch + RING - 1);
         const char* wb = smem + ((ch - ch_lo) % RING) * kChunk;
         f32x4 acc[RB][4];
@@ -293,8 +306,14 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
             float sc[4][4], sh[4][4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const f32x4 s4 = *(const f32x4*)&s_scale[n0 + 16 * j + 4 * grp];
-                const f32x4 h4 = *(const f32x4*)&s_shift[n0 + 16 * j + 4 * grp];
+                f32x4 s4, h4;
+                if constexpr (kSsLds) {
+                    s4 = *(const f32x4*)&s_scale[n0 + 16 * j + 4 * grp];
+                    h4 = *(const f32x4*)&s_shift[n0 + 16 * j + 4 * grp];
+                } else {
+                    s4 = gs4[j];
+                    h4 = gh4[j];
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     sc[j][r] = s4[r];
