@@ -416,8 +416,9 @@ __global__ __launch_bounds__(256) void conv_gemm_narrow(ConvGemmParams p) {
 // and of 4 weight rows -- the weight rows stay in L1/L2 for every wave), the MFMA k order of
 // conv_gemm_f32 (v_mfma_f32_16x16x4_f32 s = 0..3 over the 16-deep step, lane group c holding
 // k = 16 kt + 4 c + s), so the same bits.  conv_gemm_f32 ran these on 128 x 128 tiles: 64 of
-// them at B = 8,192 windows, a 64-step K loop with a barrier per step on 64 CUs: 93 vs 54 us.
-// From 256 tiles of 128 rows on, the tile kernel stays ahead (B = 65,536: 0.164 vs 0.185 ms).
+// them at B = 8,192 windows, a 64-step K loop with a barrier per step on 64 CUs: 93 vs 54 us,
+// and 38 us with an 8-step operand ring (profiles/r04final_narrow_shrink_ring_ab.txt).  From 256
+// tiles of 128 rows on, the tile kernel keeps up (B = 65,536: 0.167 vs 0.163 ms narrow).
 __global__ __launch_bounds__(64) void conv_gemm_f32_narrow(ConvGemmParams p) {
     const int lane = threadIdx.x;
     const int c = lane >> 4, r = lane & 15;
@@ -437,27 +438,32 @@ __global__ __launch_bounds__(64) void conv_gemm_f32_narrow(ConvGemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nk = p.K / 16;
-    f32x4 a = mv ? *(const f32x4*)arow : f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 w[4];
+    // a ring of kDepth K-steps of operands in flight: one step's 16 MFMAs (~130 cycles) are far
+    // shorter than a global load, so with one step of prefetch the loop waited a load latency
+    // per step (B = 8,192: 54 us for 0.9 GFLOP)
+    constexpr int kDepth = 8;
+    f32x4 ab[kDepth], wb[kDepth][4];
+    auto load_step = [&](int kt, f32x4& a, f32x4 (&w)[4]) __attribute__((always_inline)) {
+        a = mv ? *(const f32x4*)(arow + 16 * kt) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = nv[j] ? *(const f32x4*)wrow[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
-        // the next step's operands in flight under this step's 16 MFMAs
-        const bool more = kt + 1 < nk;
-        f32x4 an = f32x4{0.f, 0.f, 0.f, 0.f}, wn[4] = {an, an, an, an};
-        if (more) {
-            if (mv) an = *(const f32x4*)(arow + 16 * (kt + 1));
+        for (int j = 0; j < 4; ++j) w[j] = nv[j] ? *(const f32x4*)(wrow[j] + 16 * kt) : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (nv[j]) wn[j] = *(const f32x4*)(wrow[j] + 16 * (kt + 1));
+    for (int d = 0; d < kDepth; ++d)
+        if (d < nk) load_step(d, ab[d], wb[d]);
+    for (int kt0 = 0; kt0 < nk; kt0 += kDepth) {
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d) {
+            const int kt = kt0 + d;
+            if (kt < nk) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab[d][s], wb[d][j][s], acc[0][j], 0, 0, 0);
+                if (kt + kDepth < nk) load_step(kt + kDepth, ab[d], wb[d]);
+            }
         }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], w[j][s], acc[0][j], 0, 0, 0);
-        a = an;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = wn[j];
     }
     epilogue_scalar<float, 1>(p, acc, m0, 0, lane);
 }
@@ -469,8 +475,10 @@ bool getenv_flag_off(const char* name) {
 }
 
 bool f32_narrow_eligible(const ConvGemmParams& p) {
-    return p.N <= 64 && p.M < 256 * BM && !p.R && p.Ktap == p.K && p.K % 16 == 0 && p.K <= p.Kp && p.lda % 4 == 0 &&
-           p.Kp % 4 == 0 && aligned(p.A, 16) && aligned(p.W, 16) && getenv_flag_off("VP3D_F32_NARROW");
+    const char* e = getenv("VP3D_F32_NARROW");  // 0: never, 2: at any M (measurement)
+    const bool any_m = e && e[0] == '2';
+    return p.N <= 64 && (p.M < 256 * BM || any_m) && !p.R && p.Ktap == p.K && p.K % 16 == 0 && p.K <= p.Kp &&
+           p.lda % 4 == 0 && p.Kp % 4 == 0 && aligned(p.A, 16) && aligned(p.W, 16) && getenv_flag_off("VP3D_F32_NARROW");
 }
 
 bool narrow_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute) {
