@@ -529,8 +529,9 @@ hipError_t launch_rb_nt(const ConvGemmParams& p_in, const GatherSrc& g, int nks,
 // Row blocks of 16 per wave (RB): more rows per wave amortise each weight chunk's
 // fragment reads and the per-workgroup prologue; LDS is 3 weight chunks + RB * 8 KB of
 // output staging per workgroup, and 2 workgroups per CU need <= 80 KB.  RB = 4 for
-// K + 2 <= 128 (80 KB, 196-209 VGPRs: 2 waves per SIMD), else 2 (the camera concat,
-// K = 138: 76 KB).  Measured on the config-4 shape (B = 65,536 windows, gathered, bf16,
+// K + 2 <= 128 (80 KB, 196-209 VGPRs: 2 waves per SIMD); the camera concat (K = 138, 5
+// k-slabs) RB = 4 with a 2-chunk ring (72 KB, 212 VGPRs): config-3 fp16 expand 2.30 vs 2.57 ms
+// with RB 2 and 3 chunks (profiles/r04final_concat_expand_rb4_ab.txt).  Measured on the config-4 shape (B = 65,536 windows, gathered, bf16,
 // tools/ubench/expand_check): RB 4 -> 2.07 ms, 2 -> 2.25, 1 -> 2.74; the previous
 // kernel (BN in the epilogue, weights staged through VGPRs, a full drain per chunk)
 // took 3.12 ms.
@@ -554,7 +555,7 @@ hipError_t launch_t(const ConvGemmParams& p, const GatherSrc& g, int nks, hipStr
 #endif
     if (nks <= 4)
         return nt ? launch_rb_nt<CT, 4, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 4, GATHER, false>(p, g, nks, s);
-    return nt ? launch_rb_nt<CT, 2, GATHER, true>(p, g, nks, s) : launch_rb_nt<CT, 2, GATHER, false>(p, g, nks, s);
+    return nt ? launch_rb_nt<CT, 4, GATHER, true, 2>(p, g, nks, s) : launch_rb_nt<CT, 4, GATHER, false, 2>(p, g, nks, s);
 }
 
 }  // namespace
