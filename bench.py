@@ -17,8 +17,11 @@ At N = 1 the line also carries, each with its own roofline, parity and CPU basel
   batch_sweep_poses_per_s   B = 1,024 / 8,192 / 65,536 in f16x3 and bf16
   config3       trajectory-conditioned windows (K.E + gather + concat in the step): fp16,
                 f16x3, fp32
-  config5       causal streaming, fp16: the hipGraph-pipelined step and one frame in flight
-                (serve latency p50 / p90 / p99)
+  config5       causal streaming, fp32 (exact weights, the north-star gate) and fp16 (config 5's
+                dtype): the hipGraph-pipelined step and one frame in flight (serve latency
+                p50 / p90 / p99)
+  sequence      the dilated TemporalModel over one 65,778-frame sequence (run.py --evaluate's
+                shape) in f16x3 and fp32 (the gate) and bf16, with ΔMPJPE vs the oracle
 Besides the JSON contract fields the line carries
   roofline      dominant kernel (block-1 k3 conv GEMM) FLOP per launch / its average
                 HIP-event duration on the launch stream during the timed steps; traffic =
@@ -121,11 +124,12 @@ def stream_traffic(mode):
 
 
 def stream_main(args, world, rank, dev, emit=True):
-    """Config 5: causal TemporalModel, one frame in / one pose out per step.  16-bit
-    weights: a graph of Q steps is ONE persistent launch -- by default the layer-pipelined
-    form (each CU runs one layer with its weights in VGPRs, the frames of the graph flow
-    through the layer groups; VP3D_STREAM_MODE=persist: every CU runs every layer with its
-    weights in LDS); fp32: 10 GEMV launches per step."""
+    """Config 5: causal TemporalModel, one frame in / one pose out per step.  A graph of Q
+    steps is ONE persistent launch -- by default the layer-pipelined form (each CU runs one
+    layer with its weights in VGPRs as f32: the exact fp32 weights for --dtype fp32, 16-bit
+    ones widened for fp16 / bf16; the frames of the graph flow through the layer groups;
+    VP3D_STREAM_MODE=persist: every CU runs every layer with its 16-bit weights in LDS,
+    =launches: 10 GEMV launches per step)."""
     from common.models.TemporalModel import TemporalModel
     from oracle.temporal_ref import lifter_forward
     from vp3d_amd import synth
@@ -215,8 +219,8 @@ def stream_main(args, world, rank, dev, emit=True):
 
     def mp(a):
         return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
-    cpu = None
-    if args.cpu_seconds > 0:
+    cpu = getattr(args, "stream_cpu_baseline", None)
+    if cpu is None and args.cpu_seconds > 0:
         win = xp[:, :RF_FULL].contiguous()
         cpu = cpu_baseline(lambda: lifter_forward(sd, win, FW, causal=True), 1, "poses/s",
                            "single-frame causal steps (one 243-frame window through the torch-CPU "
@@ -235,9 +239,9 @@ def stream_main(args, world, rank, dev, emit=True):
                                   "persist": " (one persistent launch: every CU runs every layer, weights in LDS)",
                                   "launches": " (10 GEMV launches per step)"}[mode],
                    "frames_per_step": 1, "steps_per_graph": G, "mode": mode, "parallelism": f"replicas{world}"},
-        # the bound that applies: with the weights resident on chip (pipe: VGPRs, persist: LDS)
-        # a step is FMA work (f16 x f32 + f32, v_fma_mix_f32) spread over the CUs and chained
-        # through 10 layer hand-offs -- priced here against the f32 vector FMA peak; the
+        # the bound that applies: with the weights resident on chip (pipe: f32 in VGPRs,
+        # persist: 16-bit in LDS) a step is f32 FMA work (v_pk_fma_f32) spread over the CUs and
+        # chained through 10 layer hand-offs -- priced here against the f32 vector FMA peak; the
         # weight-streaming (HBM) view is kept beside it for the GEMV form
         "roofline": {"bound": "valu" if mode != "launches" else "hbm",
                      "kernel": {"pipe": "stream_pipe_kernel", "persist": "stream_persist_kernel",
@@ -251,9 +255,10 @@ def stream_main(args, world, rank, dev, emit=True):
                      "avg_step_us": round(step_s * 1e6, 3),
                      "note": ("achieved = the step's algorithmic FLOP (2 x MACs of the 10 convs) / the pipelined "
                               "step time (frames of a 64-step graph flowing through the layer groups); peak = "
-                              "the f32 vector peak (157.3 TF spec; the unpacked v_fma_mix_f32 the kernel issues "
-                              "runs at half of it). The per-frame floor is the hand-off chain: one frame crosses "
-                              "10 layer groups (serve_latency_us)." if mode != "launches" else
+                              "the f32 vector peak (157.3 TF spec, packed v_pk_fma_f32 -- the instruction the "
+                              "kernel issues, on f32 weights resident in VGPRs). The per-frame floor is the "
+                              "hand-off chain: one frame crosses 10 layer groups (serve_latency_us)."
+                              if mode != "launches" else
                               "weights re-read every step: HBM-bound GEMVs"),
                      "hbm_view": {"bytes_per_step": step_bytes, "achieved_GBps": round(achieved, 1),
                                   "frac_of_8TBps": round(achieved / 8000.0, 4)}},
@@ -272,7 +277,10 @@ def stream_main(args, world, rank, dev, emit=True):
         "serve_python_latency_us": round(float(np.median(serve_py)), 2) if serve_py else None,
         "eager_step_latency_us": round(float(np.median(lat)), 2),
         "parity": {"frames": T, f"{args.dtype}_max_coord_delta_mm": float(np.abs(outs - ref).max()) * 1e3,
-                   f"{args.dtype}_mpjpe_delta_mm": abs(mp(outs) - mp(ref)) * 1e3},
+                   f"{args.dtype}_mpjpe_delta_mm": abs(mp(outs) - mp(ref)) * 1e3,
+                   "meets_north_star_1e-4mm": bool(abs(mp(outs) - mp(ref)) * 1e3 <= 1e-4),
+                   "reference": "oracle/temporal_ref.py on the whole edge-padded sequence, causal "
+                                "(generators.py:193-198, TemporalModel.py:126-138)"},
     }
     if cpu:
         out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
@@ -372,6 +380,15 @@ def train_main(args, world, rank, dev):
                    "parallelism": f"dp{world}" + (" (gradient all_reduce, RCCL)" if world > 1 else "")},
         "flop_per_window": fwd + wg + dg,
         "tflops_effective": round(flop_step * world * args.steps / dt / 1e12, 2),
+        # the step is a chain of f32 GEMMs (forward, dgrad, wgrad of every conv on the f32 MFMA)
+        # plus HBM-bound BN / ReLU / dropout / Adam passes; priced as a whole against the f32
+        # MFMA peak (per GPU), the GEMM-only share of the time is in profiles/ (rocprofv3)
+        "roofline": {"bound": "mfma", "kernel": "whole training step (all launches)",
+                     "achieved": round(flop_step * args.steps / dt / 1e12, 2), "peak": 157.3,
+                     "unit": "TFLOP/s", "frac": round(flop_step * args.steps / dt / 1e12 / 157.3, 4),
+                     "traffic": None,
+                     "note": "algorithmic FLOP of the step (2 x MACs of forward + weight and input gradients, "
+                             "BN / dropout / Adam excluded) / the step's wall time, per GPU"},
         "loss_last": float(loss.item()),
     }
     if args.cpu_seconds > 0:
@@ -480,81 +497,109 @@ def seq_main(args, world, rank, dev):
     print(json.dumps(out), flush=True)
 
 
-def sequence_main(args, world, rank, dev):
+class SequenceCase:
     """Sequence mode (SURVEY.md §8(d) "also report"): the dilated TemporalModel over one
-    long edge-padded sequence, the run.py --evaluate shape (UnchunkedGenerator, B = 1,
-    T_out + 242 frames in, T_out poses out); bf16 by default.  FLOP(T_out) =
+    long edge-padded sequence, the run.py --evaluate shape (run.py:697-711: UnchunkedGenerator,
+    B = 1, T_out + 242 frames in, T_out poses out).  FLOP(T_out) =
     2 * (16,933,888 * T_out + 2,591,981,568)."""
-    from common.models.TemporalModel import TemporalModel
-    from oracle.temporal_ref import lifter_forward
-    from vp3d_amd import synth
 
-    model = TemporalModel(JOINTS, 2, JOINTS, FW, channels=CHANNELS)
-    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    model.eval().cuda().set_compute_dtype(args.dtype)
-    RF = model.receptive_field()
-    T_out = args.batch
-    x = synth_windows(1, T_out + RF - 1, JOINTS, 1000 + rank, dev)
-    lifter = model.native_lifter(dev)
-    lifter.reserve(1, T_out + RF - 1, args.dtype)
-    y = torch.empty((1, T_out, JOINTS, 3), device=dev)
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            lifter.forward(x, args.dtype, out=y)
-        torch.cuda.synchronize()
-        lifter.profile(True)
-        lifter.profile_reset()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            lifter.forward(x, args.dtype, out=y)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        dt = time.perf_counter() - t0
-        lifter.profile(False)
-    prof = lifter.profile_read()
+    def __init__(self, T_out, rank, dev):
+        from common.models.TemporalModel import TemporalModel
+        from vp3d_amd import synth
+        model = TemporalModel(JOINTS, 2, JOINTS, FW, channels=CHANNELS)
+        self.sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()], seed=0)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in self.sd.items()})
+        model.eval().cuda()
+        self.RF = model.receptive_field()
+        self.T_out = T_out
+        self.x = synth_windows(1, T_out + self.RF - 1, JOINTS, 1000 + rank, dev)
+        self.lifter = model.native_lifter(dev)
+        self.y = torch.empty((1, T_out, JOINTS, 3), device=dev)
+        self.flop_step = 2 * (16933888 * T_out + 2591981568)
+        self._ref = None
+
+    def run(self, dtype, steps, warmup, settle_s, world):
+        self.lifter.reserve(1, self.T_out + self.RF - 1, dtype)
+        lifter, x, y = self.lifter, self.x, self.y
+
+        def step():
+            lifter.forward(x, dtype, out=y)
+        with torch.no_grad():
+            return profiled_run(lifter, step, steps, warmup, settle_s, world)
+
+    def parity(self, P=256):
+        """The first P output frames (a time shard: inputs [0, P + RF - 1)) vs the oracle."""
+        from oracle.temporal_ref import lifter_forward
+        from vp3d_amd import synth
+        P = min(P, self.T_out)
+        if self._ref is None:
+            ref = lifter_forward(self.sd, self.x[:, :P + self.RF - 1].cpu(), FW).numpy()
+            gt = synth.gt_poses(3, "seq_gt", P, JOINTS).reshape(ref.shape)
+            self._ref = (ref, gt)
+        ref, gt = self._ref
+        got = self.y[:, :P].cpu().numpy()
+
+        def mp(a):
+            return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
+        return {"frames_checked": P, "mpjpe_delta_mm": abs(mp(got) - mp(ref)) * 1e3,
+                "max_coord_delta_mm": float(np.abs(got - ref).max()) * 1e3,
+                "meets_north_star_1e-4mm": bool(abs(mp(got) - mp(ref)) * 1e3 <= 1e-4)}
+
+    def leg(self, dtype, steps, warmup, settle_s, world=1):
+        dt, per_layer, dom = self.run(dtype, steps, warmup, settle_s, world)
+        value = world * self.T_out * steps / dt
+        r = roofline_of(dom, PEAK_TFLOPS[dtype])
+        if dtype == "f16x3":
+            r["peak_note"] = "f16 dense MFMA peak / 3: three f16 products per algorithmic multiply-add"
+        return dt, {"value": round(value, 2), "unit": "poses/s", "steps": steps,
+                    "ms_per_step": round(dt / steps * 1e3, 4),
+                    "tflops_effective": round(value / self.T_out * self.flop_step / 1e12, 2),
+                    "roofline": r, "per_layer_ms": per_layer, **self.parity()}
+
+    def cpu_baseline(self, seconds):
+        from oracle.temporal_ref import lifter_forward
+        Tc = 2048
+        xc = self.x[:, :Tc + self.RF - 1].cpu()
+        sd = self.sd
+        return cpu_baseline(lambda: lifter_forward(sd, xc, FW), Tc, "poses/s",
+                            f"one sequence of {Tc + self.RF - 1} frames -> {Tc} poses per run through "
+                            "oracle/temporal_ref.py (torch-CPU, fp32)", target_s=seconds / 5)
+
+    def close(self):
+        self.lifter.close()
+        self.x = self.y = None
+
+
+def sequence_main(args, world, rank, dev):
+    """--sequence: the dilated TemporalModel over one long sequence as the main line (bf16 by
+    default; --dtype f16x3 / fp32 for the north-star gate)."""
+    case = SequenceCase(args.batch, rank, dev)
+    dt, leg = case.leg(args.dtype, args.steps, args.warmup, args.settle_seconds, world)
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     if rank != 0:
         return
+    T_out = case.T_out
     value = world * T_out * args.steps / dt
-    flop_step = 2 * (16933888 * T_out + 2591981568)
-    dom = max(prof, key=lambda r: r["ms_total"])
-    dom_ms = dom["ms_total"] / max(dom["launches"], 1)
-    names = ["expand"] + [f"block{(i // 2) + 1}_{'k3' if i % 2 == 0 else '1x1'}"
-                          for i in range(2 * (len(FW) - 1))] + ["shrink"]
-    # parity on the first 256 output frames (a time shard: inputs [0, 256 + RF - 1))
-    P = min(256, T_out)
-    ref = lifter_forward(sd, x[:, :P + RF - 1].cpu(), FW).numpy()
-    got = y[:, :P].cpu().numpy()
     out = {
         "metric": "3D poses/sec, dilated TemporalModel sequence mode (243-frame RF, 17 joints, 1024ch)",
         "value": round(value, 2), "unit": "poses/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded random-walk sequence, counter-hash weights)",
-        "config": {"workload": f"TemporalModel (dilated) on one sequence of {T_out + RF - 1} frames -> {T_out} poses "
-                               "(run.py --evaluate, UnchunkedGenerator)", "poses_per_step": T_out,
+        "config": {"workload": f"TemporalModel (dilated) on one sequence of {T_out + case.RF - 1} frames -> {T_out} "
+                               "poses (run.py --evaluate, UnchunkedGenerator)", "poses_per_step": T_out,
                    "parallelism": f"dp{world} (independent sequences)"},
-        "flop_per_step": flop_step, "tflops_effective": round(value / T_out * flop_step / 1e12, 2),
-        "roofline": {"bound": "mfma", "kernel": f"conv_gemm ({names[dom['layer']]})",
-                     "achieved": round(dom["flop"] / (dom_ms * 1e-3) / 1e12, 2), "peak": PEAK_TFLOPS[args.dtype],
-                     "unit": "TFLOP/s", "frac": round(dom["flop"] / (dom_ms * 1e-3) / 1e12 / PEAK_TFLOPS[args.dtype], 4),
-                     "traffic": None, "avg_launch_ms": round(dom_ms, 4), "flop_per_launch": dom["flop"]},
-        "per_layer_ms": {names[r["layer"]]: round(r["ms_total"] / max(r["launches"], 1), 4) for r in prof},
-        "parity": {"frames_checked": P, "max_coord_delta_mm": float(np.abs(got - ref).max()) * 1e3},
+        "flop_per_step": case.flop_step, "tflops_effective": round(value / T_out * case.flop_step / 1e12, 2),
+        "roofline": leg["roofline"], "per_layer_ms": leg["per_layer_ms"],
+        "parity": {k: leg[k] for k in ("frames_checked", "mpjpe_delta_mm", "max_coord_delta_mm",
+                                       "meets_north_star_1e-4mm")},
     }
     if args.cpu_seconds > 0:
-        Tc = 2048
-        xc = x[:, :Tc + RF - 1].cpu()
-        out["cpu_baseline"] = cpu_baseline(lambda: lifter_forward(sd, xc, FW), Tc, "poses/s",
-                                           f"one sequence of {Tc + RF - 1} frames -> {Tc} poses per run through "
-                                           "oracle/temporal_ref.py (torch-CPU, fp32)", target_s=args.cpu_seconds / 5)
+        out["cpu_baseline"] = case.cpu_baseline(args.cpu_seconds)
+        out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+    case.close()
     print(json.dumps(out), flush=True)
 
 
@@ -613,7 +658,12 @@ def cpu_baseline(run_once, units_per_run, unit, sample_desc, repeats=5, target_s
             rates.append(reps * units_per_run / (time.perf_counter() - t))
     finally:
         torch.set_num_threads(prev)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {"value": round(float(np.median(rates)), 3), "unit": unit, "cores": threads, "kind": "port",
+            "affinity_cpus": affinity,
             "sample": f"{sample_desc}; median of {repeats} runs of {reps} x {units_per_run} after 2 warm-ups "
                       f"({sum(reps * units_per_run / r for r in rates):.1f} s timed)",
             "runs": [round(r, 3) for r in rates], "runs_order": "time order", **info,
@@ -948,10 +998,31 @@ def windows_main(args, world, rank, dev):
         out["config3"] = leg3
         c3.close()
         del c3
-        # ---- config 5: causal streaming (fp16, hipGraph of 64 steps; serve latency) ----
-        a5 = argparse.Namespace(**vars(args))
-        a5.dtype, a5.steps, a5.warmup = "fp16", 64 * 40, 64 * 4
-        out["config5"] = stream_main(a5, 1, 0, dev, emit=False)
+        # ---- sequence mode (run.py --evaluate's path): f16x3 and fp32 at the gate, bf16 ----
+        sq = SequenceCase(65536, 0, dev)
+        legs_s = {"workload": f"TemporalModel (dilated) on one sequence of {65536 + sq.RF - 1} frames -> 65,536 "
+                              "poses per step (run.py:697-711, UnchunkedGenerator edge padding)",
+                  "flop_per_step": sq.flop_step}
+        for dl, ks in (("f16x3", max(5, args.steps // 2)), ("fp32", max(3, args.steps // 4)),
+                       ("bf16", max(5, args.steps // 2))):
+            legs_s[dl] = sq.leg(dl, ks, 1, 0.3)[1]
+        if args.cpu_seconds > 0:
+            legs_s["cpu_baseline"] = sq.cpu_baseline(args.cpu_seconds)
+            for dl in ("f16x3", "fp32", "bf16"):
+                legs_s[dl]["speedup_vs_cpu"] = round(legs_s[dl]["value"] / legs_s["cpu_baseline"]["value"], 1)
+        out["sequence"] = legs_s
+        sq.close()
+        del sq
+        # ---- config 5: causal streaming, hipGraph of 64 steps + serve latency: fp32 (exact
+        # weights resident, the north-star gate) and fp16 (config 5's named dtype) ----
+        c5 = {}
+        for d5 in ("fp32", "fp16"):
+            a5 = argparse.Namespace(**vars(args))
+            a5.dtype, a5.steps, a5.warmup = d5, 64 * 40, 64 * 4
+            if "fp32" in c5:
+                a5.stream_cpu_baseline = c5["fp32"].get("cpu_baseline")
+            c5[d5] = stream_main(a5, 1, 0, dev, emit=False)
+        out["config5"] = c5
     print(json.dumps(out), flush=True)
 
 

@@ -40,7 +40,8 @@ def build_parser():
     a('--by-subject', action='store_true', help='break down error by subject (on evaluation)')
     a('--export-training-curves', action='store_true', help='save training curves (not on this path)')
     # Model selection / learning (:32-38)
-    a('--use-model', dest='model_name', default='FCN', type=str, help='only FCN runs on this path')
+    a('--use-model', dest='model_name', default='FCN', type=str, help='FCN (TemporalModel), Transformer (CoupledTransformer) or LSTM-Coupled '
+      '(CoupledLSTM; --evaluate runs the trajectory lifters over sliding windows)')
     a('-e', '--epochs', default=60, type=int, metavar='N', help='number of training epochs')
     a('-b', '--batch-size', default=1024, type=int, metavar='N', help='batch size in terms of predicted frames')
     a('-lr', '--learning-rate', default=0.001, type=float, metavar='LR', help='initial learning rate')

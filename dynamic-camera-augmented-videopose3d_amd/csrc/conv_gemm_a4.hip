@@ -437,30 +437,41 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         });
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         pinned_barrier();
-        if (tid == 0) __hip_atomic_fetch_add(p.sk_flag + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0 && !p.sk_drop) __hip_atomic_fetch_add(p.sk_flag + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
+    // the owner's helpers that delivered: S, or 1 after a timed-out wait (their partial sums
+    // are then skipped and the fault reported through sk_err, never added half-written)
+    __shared__ int s_sk_ok;
+    int sk_n = S;
     auto owner_wait = [&](int si) __attribute__((always_inline)) {
         if (tid == 0) {
+            int ok = 1;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             while (__hip_atomic_load(p.sk_flag + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > p.sk_spin) {
+                    ok = 0;
+                    if (p.sk_err) __hip_atomic_store(p.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
             }
+            s_sk_ok = ok;
         }
         pinned_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        sk_n = __builtin_amdgcn_readfirstlane(s_sk_ok) ? S : 1;
     };
     // v (the accumulators of block R as two pairs) += the helpers' values of that block
     auto owner_add = [&](auto r_c, int si, f32x2 (&v)[2]) __attribute__((always_inline)) {
         constexpr int R = decltype(r_c)::value;
-        for (int q = 1; q < S; ++q) {
+        for (int q = 1; q < sk_n; ++q) {
             const f32x4 pr = *(const f32x4*)(part_ptr(si, q) + (R / 4) * 256);
             v[0] = v[0] + f32x2{pr[0], pr[1]};
             v[1] = v[1] + f32x2{pr[2], pr[3]};
         }
     };
     auto owner_done = [&](int si) __attribute__((always_inline)) {
-        if (tid == 0) __hip_atomic_store(p.sk_flag + si, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_fetch_sub(p.sk_flag + si, S - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto epi_fast = [&](auto h_c, bool with_res, int em0, int en0, __amdgpu_buffer_rsrc_t y_rsrc, int own_si) __attribute__((always_inline)) {
         constexpr int H = decltype(h_c)::value;
@@ -972,11 +983,15 @@ static int a4_cus() {
 // 1x1 0.100 vs 0.061 ms).  Needs the handle's workspace (sk_part); VP3D_A4_SPLIT=0
 // (measurement; read at every launch) turns it off, 2 takes it wherever it fits.  Returns the
 // plan in q.sk_* (sk_split 0: none).
-static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk) {
+static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk, bool need_ws = true) {
     q.sk_split = q.sk_full = q.sk_left = 0;
     const char* e = getenv("VP3D_A4_SPLIT");
     const int mode = e ? atoi(e) : 1;
-    if (mode == 0 || !q.sk_part || !q.sk_flag) return;
+    if (mode == 0 || (need_ws && (!q.sk_part || !q.sk_flag))) return;
+    const char* d = getenv("VP3D_A4_SPLIT_DROP");
+    q.sk_drop = d && atoi(d) != 0;
+    const char* sp = getenv("VP3D_A4_SPLIT_SPIN_TICKS");
+    q.sk_spin = sp ? strtoull(sp, nullptr, 10) : kSplitSpinTicks;
     const int ncu = a4_cus();
     if (ncu <= 0 || ncu > 256) return;  // the workspace holds one round of 256 slots
     if (mode == 1 && (nk < 64 || ntiles >= 8 * ncu)) return;
@@ -993,6 +1008,13 @@ static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk) {
 
 // the tile count from which a4 is the kernel of a 16-bit layer (fewer: q64 / the 128 x 128
 // kernel), unless a split plan fills the chip (config 4's block 4 at N = 8: 128 tiles)
+bool conv_gemm_a4_would_split(const ConvGemmParams& p) {
+    const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+    ConvGemmParams q = p;
+    a4_split_plan(q, ntiles, p.Kp / GK, false);
+    return q.sk_split > 1;
+}
+
 bool conv_gemm_a4_fills(const ConvGemmParams& p) {
     const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
     if (ntiles >= 384) return true;

@@ -474,8 +474,9 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     }
 }
 
-// resident workgroup slots per launch: two per CU (__launch_bounds__(256, 2); the
-// NKS = 5 variants hold one, and then the split round below is two rounds of half the size)
+// resident workgroup slots per launch: two per CU (__launch_bounds__(256, 2)) for every
+// variant -- the camera-concat NKS = 5 one included since its RB 4 / 2-chunk weight ring
+// (72 KB of LDS)
 static int exp_slots() {
     static const int n = [] {
         int dev = 0, ncu = 0;

@@ -110,9 +110,14 @@ struct vp3d_handle {
     // window-gather scratch of vp3d_forward_windows when the fused expand path does not apply
     float* gather_ws = nullptr;
     size_t gather_bytes = 0;
-    // split-K workspace of conv_gemm_a4 (ConvGemmParams::sk_part / sk_flag; flags zeroed once,
-    // each owner unit resets its own)
+    // split-K workspace of conv_gemm_a4 (ConvGemmParams::sk_part / sk_flag), allocated on the
+    // first forward whose plan splits a layer; flags zeroed then, each owner unit takes its
+    // helpers' counts back out (and vp3d_sync_status re-zeroes them after a reported timeout)
     void* sk_ws = nullptr;
+    // host-mapped split-K fault word (ConvGemmParams::sk_err): set by an owner unit whose
+    // helpers did not arrive in time; checked at the next call and by vp3d_sync_status
+    unsigned* sk_err_host = nullptr;
+    unsigned* sk_err_dev = nullptr;
     // profiling
     bool profiling = false;
     uint64_t prof_mask = ~0ull;  // layers timed while profiling (bit i = layer i)

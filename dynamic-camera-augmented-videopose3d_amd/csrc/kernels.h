@@ -41,9 +41,18 @@ struct ConvGemmParams {
     // the owner unit (the first K range) adds them, in unit order, before its epilogue.
     // expand_gemm reuses sk_full / sk_split for its N split of the partial last round: row
     // blocks [0, sk_full) whole, each later one as sk_split workgroups of a channel range.
+    // A tile's flag counts its helpers in and the owner takes S - 1 back out (an atomic
+    // subtract, so a helper arriving after a timed-out owner leaves it at 0, not above).  The
+    // owner's wait is bounded (sk_spin ticks of the 100 MHz clock); on the bound it skips the
+    // helpers' partial sums and stores 1 into sk_err (host-mapped: the next call on the handle,
+    // or vp3d_sync_status, reports it) -- wrong output is never silent.  sk_drop (fault-
+    // injection tests, VP3D_A4_SPLIT_DROP=1) makes the helpers skip their count.
     float* sk_part;
     int* sk_flag;
     int sk_full, sk_split, sk_left;
+    unsigned* sk_err;
+    unsigned long long sk_spin;
+    int sk_drop;
 };
 
 // bytes of the split-K workspace a handle provides (ConvGemmParams::sk_part, then the flags)
@@ -73,6 +82,10 @@ hipError_t launch_conv_gemm_q64(const ConvGemmParams& p, Act compute, hipStream_
 bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Act compute);
 // >= 384 tiles of 256 x 256, or fewer that a split-K plan spreads over every CU
 bool conv_gemm_a4_fills(const ConvGemmParams& p);
+// true when the launch of this layer on a4 would split its partial last round (the host then
+// provides the split-K workspace, sk_part / sk_flag; without it the tiles run whole)
+bool conv_gemm_a4_would_split(const ConvGemmParams& p);
+constexpr unsigned long long kSplitSpinTicks = 100000000ull;  // 1 s of the 100 MHz clock
 hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t stream);
 // Split-fp16 mode of conv_gemm_a4 (the q64 contract above, N % 256 == 0, >= 384 tiles); the same
 // bits as conv_gemm_q64_x3.

@@ -28,7 +28,10 @@
 //     reduced across the wave (DPP within 16-lane rows, then the 4 row sums).
 //   * expand ("lane per channel"): lane L owns one output channel and its whole weight row
 //     (K = 3 * 34 = 102, padded to 128); the 3-frame input vector is an LDS broadcast.
-// f16 weights feed v_fma_mix_f32 (f16 x f32 + f32, exact widening); activations stay f32.
+// Weights are held as f32 pairs in VGPRs (16-bit weights widened exactly once at launch; the
+// exact-fp32 form, WT = float, loads them as they are -- the same registers either way) and
+// every dot product runs on v_pk_fma_f32 with f32 activations, so the fp32 form differs from
+// the reference only by the order of its f32 sums.
 //
 // Block b's k-conv is split by tap (as in stream_persist.hip): the newest tap completes
 // output t; the older taps' products of x(t) go into a wave-private ring of partial sums
@@ -65,6 +68,17 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 template <typename WT>
 __device__ __forceinline__ f2 widen2(uint32_t w) {
     return f2{lo16<WT>(w), hi16<WT>(w)};
+}
+
+// weight pair i of a row (elements 2i, 2i + 1) as f32: a widened 16-bit pair, or two f32 as stored
+template <typename WT>
+__device__ __forceinline__ f2 wpair(const WT* row, int i) {
+    if constexpr (sizeof(WT) == 4) {
+        const float2 v = *(const float2*)(row + 2 * i);
+        return f2{v.x, v.y};
+    } else {
+        return widen2<WT>(((const uint32_t*)row)[i]);
+    }
 }
 
 template <int CTRL>
@@ -237,9 +251,9 @@ __device__ __forceinline__ void load_rows(f2 (&w)[NT][CW][KS / 2], const WT* W, 
 #pragma unroll
             for (int i = 0; i < KS / 2; ++i) w[t][j][i] = f2{0.f, 0.f};
             if (c < c_hi && t < taps) {
-                const uint32_t* src = (const uint32_t*)(W + (int64_t)c * Kp + t * C + lane * KS);
+                const WT* src = W + (int64_t)c * Kp + t * C + lane * KS;
 #pragma unroll
-                for (int i = 0; i < KS / 2; ++i) w[t][j][i] = widen2<WT>(src[i]);
+                for (int i = 0; i < KS / 2; ++i) w[t][j][i] = wpair<WT>(src, i);
             }
         }
 }
@@ -369,9 +383,9 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
 #pragma unroll
         for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = f2{0.f, 0.f};
         if (c < c_hi) {
-            const uint32_t* src = (const uint32_t*)((const WT*)Wr + (int64_t)c * K0);
+            const WT* src = (const WT*)Wr + (int64_t)c * K0;
 #pragma unroll
-            for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = widen2<WT>(2 * i < K0 ? src[i] : 0u);  // K0 <= kPipeExpandK
+            for (int i = 0; i < kPipeExpandK / 2; ++i) w[i] = 2 * i < K0 ? wpair<WT>(src, i) : f2{0.f, 0.f};  // K0 <= kPipeExpandK
         }
         const float sc = c < c_hi ? scl[c - c_lo] : 0.f, sh = c < c_hi ? scl[kPipeMaxCh + c - c_lo] : 0.f;
         // thread i < cin0 owns input element i: frames t-1, t-2 of it stay in registers (hist
@@ -661,6 +675,8 @@ hipError_t launch_stream_pipe(const StreamPipeParams& p, Act wtype, int lds_byte
     else if (wtype == Act::F16 && KS == 4) VP3D_PIPE(_Float16, 4);
     else if (wtype == Act::BF16 && KS == 16) VP3D_PIPE(__bf16, 16);
     else if (wtype == Act::BF16 && KS == 4) VP3D_PIPE(__bf16, 4);
+    else if (wtype == Act::F32 && KS == 16) VP3D_PIPE(float, 16);
+    else if (wtype == Act::F32 && KS == 4) VP3D_PIPE(float, 4);
     else return hipErrorInvalidValue;
 #undef VP3D_PIPE
     return hipGetLastError();
@@ -686,6 +702,12 @@ hipError_t stream_pipe_prepare(Act wtype, int C, int lds_bytes) {
     } else if (wtype == Act::BF16 && C == 256) {
         f[0] = (const void*)stream_pipe_kernel<__bf16, 4, false>;
         f[1] = (const void*)stream_pipe_kernel<__bf16, 4, true>;
+    } else if (wtype == Act::F32 && C == 1024) {
+        f[0] = (const void*)stream_pipe_kernel<float, 16, false>;
+        f[1] = (const void*)stream_pipe_kernel<float, 16, true>;
+    } else if (wtype == Act::F32 && C == 256) {
+        f[0] = (const void*)stream_pipe_kernel<float, 4, false>;
+        f[1] = (const void*)stream_pipe_kernel<float, 4, true>;
     } else {
         return hipErrorInvalidValue;
     }

@@ -357,10 +357,6 @@ int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
     // three rotating activation buffers + (16-bit path) the packed expand-conv rows
     const size_t need = 3 * rows * h->cfg.channels * esize(dtype) +
                         (dtype == VP3D_DTYPE_F32 ? 0 : rows * h->layers[0].Kp * (dtype == VP3D_DTYPE_F16X3 ? 4 : 2));
-    if (!h->sk_ws) {
-        HIP_TRY(hipMalloc(&h->sk_ws, vp3d::kSplitPartBytes + vp3d::kSplitFlagBytes));
-        HIP_TRY(hipMemset((char*)h->sk_ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitFlagBytes));
-    }
     if (need <= h->ws_bytes) return VP3D_OK;
     if (h->ws) HIP_TRY(hipFree(h->ws));
     h->ws = nullptr;
@@ -373,6 +369,41 @@ int ensure_ws(vp3d_handle* h, int B, int T, int dtype) {
 // the split-fp16 path runs every conv but the shrink on conv_gemm_q64's X3 mode
 bool x3_supported(const vp3d_handle* h) { return h->cfg.channels % 64 == 0 && h->cfg.channels <= 1024; }
 const char* x3_requirement() { return "dtype f16x3 needs channels % 64 == 0 and channels <= 1024"; }
+
+// The split-K workspace (kSplitPartBytes of partial sums + the tile flags) and the host-mapped
+// fault word, on the first layer whose a4 plan splits (not on every handle)
+int ensure_split_ws(vp3d_handle* h, hipStream_t s) {
+    if (h->sk_ws) return VP3D_OK;
+    if (!h->sk_err_host) {
+        HIP_TRY(hipHostMalloc((void**)&h->sk_err_host, 4, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer((void**)&h->sk_err_dev, h->sk_err_host, 0));
+        *(volatile unsigned*)h->sk_err_host = 0u;
+    }
+    void* ws = nullptr;
+    HIP_TRY(hipMalloc(&ws, vp3d::kSplitPartBytes + vp3d::kSplitFlagBytes));
+    const hipError_t e = hipMemsetAsync((char*)ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitFlagBytes, s);
+    if (e != hipSuccess) {
+        hipFree(ws);
+        return fail(VP3D_ERR_HIP, std::string("split-K flags: ") + hipGetErrorString(e));
+    }
+    h->sk_ws = ws;
+    return VP3D_OK;
+}
+
+// the workspace into p when a4 would split this layer (allocated then), else none
+int attach_split_ws(vp3d_handle* h, ConvGemmParams& p, hipStream_t s) {
+    if (!conv_gemm_a4_would_split(p)) return VP3D_OK;
+    const int rc = ensure_split_ws(h, s);
+    if (rc) return rc;
+    p.sk_part = (float*)h->sk_ws;
+    p.sk_flag = (int*)((char*)h->sk_ws + kSplitPartBytes);
+    p.sk_err = h->sk_err_dev;
+    return VP3D_OK;
+}
+
+constexpr const char* kSplitFaultMsg =
+    "split-K: an owner tile timed out waiting for its helper units (an earlier forward on this "
+    "handle produced wrong poses); vp3d_sync_status clears the fault";
 
 hipEvent_t get_event(vp3d_handle* h) {
     if (!h->free_events.empty()) {
@@ -438,6 +469,7 @@ int vp3d_destroy(vp3d_handle* h) {
     if (h->ws) hipFree(h->ws);
     if (h->gather_ws) hipFree(h->gather_ws);
     if (h->sk_ws) hipFree(h->sk_ws);
+    if (h->sk_err_host) hipHostFree(h->sk_err_host);
     for (auto& e : h->pending) {
         hipEventDestroy(e.a);
         hipEventDestroy(e.b);
@@ -500,6 +532,9 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         return fail(VP3D_ERR_ARG, "input of " + std::to_string(T) +
                                       " frames does not fit the receptive field of " +
                                       std::to_string(vp3d_receptive_field(h)));
+    // a split-K timeout of an earlier launch on this handle (no synchronisation: the word is
+    // host-mapped); sticky until vp3d_sync_status
+    if (h->sk_err_host && *(volatile unsigned*)h->sk_err_host) return fail(VP3D_ERR_STATE, kSplitFaultMsg);
     int rc = ensure_ws(h, B, T, dtype);
     if (rc) return rc;
 
@@ -537,8 +572,6 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         p.lda = L.cin;
         p.relu = L.relu ? 1 : 0;
         p.ldy = L.cout;
-        p.sk_part = (float*)h->sk_ws;
-        p.sk_flag = (int*)((char*)h->sk_ws + kSplitPartBytes);
         p.W = dtype == VP3D_DTYPE_F32 ? (const void*)L.w32
                                       : (dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh);
         int out_buf = -1;
@@ -623,6 +656,7 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
             if (L.residual) p.ldr = 2 * L.cout;
             // the one-wave-per-SIMD kernel where it fills the chip (VP3D_GEMM=q64 forces q64)
             const char* ge = getenv("VP3D_GEMM");
+            if ((rc = attach_split_ws(h, p, s))) return rc;
             if (!(ge && strcmp(ge, "q64") == 0) && conv_gemm_a4_x3_eligible(p, out_f32)) {
                 e = launch_conv_gemm_a4_x3(p, out_f32, s);
             } else {
@@ -680,7 +714,10 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
             p.dil = 1;
             a_type = act;
         }
-        if (!launched) e = launch_conv_gemm(p, a_type, o_type, act, s);
+        if (!launched) {
+            if (act != Act::F32 && !first && !last && (rc = attach_split_ws(h, p, s))) return rc;
+            e = launch_conv_gemm(p, a_type, o_type, act, s);
+        }
         if (e != hipSuccess)
             return fail(VP3D_ERR_HIP, std::string("conv layer ") + std::to_string(li) + ": " +
                                           hipGetErrorString(e));
@@ -732,6 +769,20 @@ int vp3d_forward_windows(vp3d_handle* h, const float* kps, int32_t f2, const flo
     g.pairs = pairs;
     g.lead = lead;
     return forward_impl(h, nullptr, B, window, y, dtype, stream, &g);
+}
+
+int vp3d_sync_status(vp3d_handle* h, void* stream) {
+    if (!h) return fail(VP3D_ERR_ARG, "handle is NULL");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    if (!h->sk_err_host || !*(volatile unsigned*)h->sk_err_host) return VP3D_OK;
+    // every launch of this handle on `stream` is done: re-zero the tile flags (a timed-out
+    // owner took back counts that never came) and clear the word, then report
+    if (h->sk_ws) {
+        HIP_TRY(hipMemsetAsync((char*)h->sk_ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitFlagBytes, (hipStream_t)stream));
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    }
+    *(volatile unsigned*)h->sk_err_host = 0u;
+    return fail(VP3D_ERR_STATE, kSplitFaultMsg);
 }
 
 int vp3d_profile_enable(vp3d_handle* h, int enable) {
@@ -824,6 +875,9 @@ struct vp3d_stream {
     int64_t posted = 0;                // host: frames posted so far (absolute)
     int64_t done_seen = 0;             // host: frames whose pose granules were all seen
     hipStream_t serve_stream = nullptr;
+    // one event per HIP stream this vp3d_stream launched on, recorded after each launch:
+    // vp3d_stream_reset waits for exactly these (not for the whole device)
+    std::vector<std::pair<hipStream_t, hipEvent_t>> launch_events;
 };
 
 namespace {
@@ -836,6 +890,17 @@ int pow2_at_least(int v) {
     int r = 1;
     while (r < v) r <<= 1;
     return r;
+}
+
+// record "this vp3d_stream's launches on s are done" (not during a graph capture)
+hipError_t mark_launched(vp3d_stream* st, hipStream_t s) {
+    for (auto& se : st->launch_events)
+        if (se.first == s) return hipEventRecord(se.second, s);
+    hipEvent_t e = nullptr;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (r != hipSuccess) return r;
+    st->launch_events.emplace_back(s, e);
+    return hipEventRecord(e, s);
 }
 
 // `steps` consecutive steps: one persistent launch (after zeroing its hand-off words), or
@@ -949,7 +1014,6 @@ bool stream_persist_setup(vp3d_stream* st, int dtype) {
 // C other than 1024 / 256, k-convs other than 3 taps, an expand wider than 128 inputs.
 bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     const vp3d_handle* h = st->h;
-    if (dtype == VP3D_DTYPE_F32) return false;
     const char* mode = getenv("VP3D_STREAM_MODE");
     if (mode && strcmp(mode, "pipe")) return false;
     const int nl = (int)h->layers.size(), nb = h->cfg.n_widths - 1, C = h->cfg.channels;
@@ -989,7 +1053,8 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     int g = 0;
     for (int l = 0; l < nl; ++l) {
         const Layer& L = h->layers[l];
-        p.W[l] = dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh;
+        p.W[l] = dtype == VP3D_DTYPE_F32 ? (const void*)L.w32
+                 : dtype == VP3D_DTYPE_BF16 ? (const void*)L.wbf : (const void*)L.wh;
         p.scale[l] = L.scale;
         p.shift[l] = L.shift;
         p.Kp[l] = L.Kp;
@@ -1000,7 +1065,7 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     p.cu0[nl] = g;
     if (g > cus) return false;
     const int lds = stream_pipe_lds_bytes(C, p.cin0, max_ring);
-    const Act wt = dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16;
+    const Act wt = dtype == VP3D_DTYPE_F32 ? Act::F32 : (dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16);
     if (lds > 160 * 1024 || stream_pipe_prepare(wt, C, lds) != hipSuccess) return false;
     st->pipe_lds = lds;
     p.state_stride = std::max(8 * max_ring * kPipeCwK, 2 * p.cin0);
@@ -1190,8 +1255,9 @@ int vp3d_stream_reset(vp3d_stream* st, void* stream) {
     if (!st) return fail(VP3D_ERR_ARG, "stream is NULL");
     if (st->serving) return fail(VP3D_ERR_STATE, "serving: vp3d_stream_serve_end first");
     // position, arrival counter and the sticky timeout word; the host mirror is cleared
-    // once no launch of this stream can still set it (launches may have gone to any stream)
-    HIP_TRY(hipDeviceSynchronize());
+    // once no launch of this stream can still set it (launches may have gone to any stream:
+    // wait for each one's last launch, not for the whole device)
+    for (auto& se : st->launch_events) HIP_TRY(hipEventSynchronize(se.second));
     HIP_TRY(hipMemsetAsync(st->frames_seen, 0, 16, (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     *(volatile unsigned*)st->err_host = 0u;
@@ -1221,6 +1287,7 @@ int vp3d_stream_step(vp3d_stream* st, const float* frame, float* pose, void* str
                                hipMemcpyDeviceToDevice, s));
     int rc = stream_launch(st, s);
     if (rc) return rc;
+    HIP_TRY(mark_launched(st, s));
     if (pose)
         HIP_TRY(hipMemcpyAsync(pose, st->out_pose + (size_t)slot * cout, 4 * cout,
                                hipMemcpyDeviceToDevice, s));
@@ -1266,6 +1333,7 @@ int vp3d_stream_graph_launch(vp3d_stream* st, void* stream) {
     if (st->serving) return fail(VP3D_ERR_STATE, "serving: post frames with vp3d_stream_serve_post");
     if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
     HIP_TRY(hipGraphLaunch(st->exec, (hipStream_t)stream));
+    HIP_TRY(mark_launched(st, (hipStream_t)stream));
     st->host_t += st->graph_steps;
     return VP3D_OK;
 }
@@ -1334,8 +1402,9 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     p.end_claim = st->end_frame + 1;
     p.idle_ticks = (unsigned long long)(idle_ms * 1e5);  // 100 MHz clock
     p.steps = 0;
-    const Act wt = st->dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16;
+    const Act wt = st->dtype == VP3D_DTYPE_F32 ? Act::F32 : (st->dtype == VP3D_DTYPE_BF16 ? Act::BF16 : Act::F16);
     HIP_TRY(launch_stream_pipe(p, wt, st->pipe_lds, s));
+    HIP_TRY(mark_launched(st, s));
     st->serving = true;
     st->serve_stream = s;
     return VP3D_OK;
@@ -1449,6 +1518,7 @@ int vp3d_stream_destroy(vp3d_stream* st) {
     hipFree(st->pipe_state);
     hipFree(st->pipe_trace);
     hipHostFree(st->err_host);
+    for (auto& se : st->launch_events) hipEventDestroy(se.second);
     delete st;
     return VP3D_OK;
 }

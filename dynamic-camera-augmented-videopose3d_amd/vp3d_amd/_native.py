@@ -43,7 +43,8 @@ MAX_BLOCKS = 8
 EXPORTS = [
     "vp3d_weight_count", "vp3d_create", "vp3d_load_weights", "vp3d_destroy",
     "vp3d_receptive_field", "vp3d_total_causal_shift", "vp3d_out_frames",
-    "vp3d_reserve", "vp3d_forward", "vp3d_forward_windows", "vp3d_profile_enable", "vp3d_layer_count",
+    "vp3d_reserve", "vp3d_forward", "vp3d_forward_windows", "vp3d_sync_status", "vp3d_profile_enable",
+    "vp3d_layer_count",
     "vp3d_profile_read", "vp3d_profile_reset", "vp3d_profile_layers", "vp3d_normalize_screen",
     "vp3d_normalize_screen_f64", "vp3d_image_coordinates", "vp3d_camera_matrices", "vp3d_world_to_camera",
     "vp3d_gather_windows", "vp3d_mpjpe_accumulate", "vp3d_pose_metrics", "vp3d_project_to_2d", "vp3d_last_error", "vp3d_abi_version",
@@ -118,6 +119,7 @@ _SIGNATURES = {
     "vp3d_forward": (_int, [_vp, _vp, _int, _int, _vp, _int, _vp]),
     "vp3d_forward_windows": (_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp, _int, _int, _int, _vp, _int, _vp]),
     "vp3d_profile_enable": (_int, [_vp, _int]),
+    "vp3d_sync_status": (_int, [_vp, _vp]),
     "vp3d_layer_count": (_int, [_vp]),
     "vp3d_profile_read": (_int, [_vp, _vp, _vp, _vp]),
     "vp3d_profile_reset": (_int, [_vp]),

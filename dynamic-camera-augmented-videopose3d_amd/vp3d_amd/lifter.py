@@ -138,6 +138,12 @@ class NativeLifter:
                 N.DTYPES[dtype], N.stream_ptr(self.device)), "vp3d_forward_windows")
         return out
 
+    def sync_status(self) -> None:
+        """Synchronise the current stream; raise RuntimeError if a launch of this lifter
+        reported a device-side fault (vp3d_sync_status: a split-K owner that timed out)."""
+        with torch.cuda.device(self.device):
+            N.check(self._lib.vp3d_sync_status(self._h, N.stream_ptr(self.device)), "vp3d_sync_status")
+
     # ---- profiling ----
     def profile(self, enable: bool) -> None:
         N.check(self._lib.vp3d_profile_enable(self._h, 1 if enable else 0))

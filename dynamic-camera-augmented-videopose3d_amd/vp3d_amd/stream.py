@@ -1,9 +1,11 @@
 """Causal streaming inference (BASELINE config 5): one 2D frame in, one 3D pose out.
 
-Wraps vp3d_stream (include/vp3d.h): with 16-bit weights a batch of steps is one
-persistent launch (csrc/stream_persist.hip: weights resident in LDS, layer outputs
-handed between CUs in-launch), with fp32 weights one GEMV launch per layer
-(csrc/stream_step.hip).  For a causal dilated TemporalModel
+Wraps vp3d_stream (include/vp3d.h): a batch of steps is one layer-pipelined persistent
+launch (csrc/stream_pipe.hip: every CU owns one layer's channel slice with its weights
+resident in VGPRs as f32 -- exact fp32 weights for dtype "fp32", 16-bit weights widened
+for "fp16" / "bf16" -- and layer outputs are handed between CUs in-launch); shapes the
+pipeline does not cover fall back to stream_persist.hip (16-bit weights in LDS) or to one
+GEMV launch per layer (csrc/stream_step.hip).  For a causal dilated TemporalModel
 (reference TemporalModel.py:79-138 with causal=True), pose k of the stream equals
 frame k of the reference's whole-sequence evaluation of the edge-padded
 sequence (UnchunkedGenerator, generators.py:193-198, causal_shift = pad).
@@ -58,8 +60,9 @@ class CausalStream:
 
     @property
     def persistent(self) -> bool:
-        """True when steps run as one persistent launch per batch (16-bit weights resident
-        in LDS); False for one GEMV launch per layer (fp32, or VP3D_STREAM_MODE=launches)."""
+        """True when steps run as one persistent launch per batch (weights resident on
+        chip: mode 'pipe' or 'persist'); False for one GEMV launch per layer
+        (VP3D_STREAM_MODE=launches, or a shape neither persistent form covers)."""
         return bool(self._lib.vp3d_stream_persistent(self._s))
 
     @property

@@ -117,6 +117,14 @@ int vp3d_reserve(vp3d_handle* h, int B, int T, int dtype);
  * Launches on `stream`; returns without synchronising. */
 int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dtype, void* stream);
 
+/* Synchronise `stream` and report a device-side fault of this handle's launches since the
+ * last call: VP3D_ERR_STATE when a split-K owner tile (conv_gemm_a4, the partial last round
+ * of small f16x3 batches) gave up waiting for its helper units -- its output was then
+ * wrong; the fault is cleared by this call.  (The next vp3d_forward* on the handle also
+ * refuses with VP3D_ERR_STATE while the fault is pending, without synchronising.)  No
+ * reference counterpart: torch raises asynchronous device errors at the next sync. */
+int vp3d_sync_status(vp3d_handle* h, void* stream);
+
 /* Eval-mode forward of B windows gathered on the fly from device-resident
  * sequences: the ChunkedGenerator batch (generators.py:102-137; edge padding of
  * pad_chunk :92-100) and the trajectory concat (CamTransformer.py:187-190) feeding
@@ -158,7 +166,8 @@ int vp3d_profile_reset(vp3d_handle* h);
  * so one step is replayable from a hipGraph. */
 typedef struct vp3d_stream vp3d_stream;
 
-/* dtype: VP3D_DTYPE_* of the weights streamed per step (f16 in config 5). */
+/* dtype: VP3D_DTYPE_* of the weights streamed per step (f16 in config 5; F32 keeps the
+ * exact fp32 weights resident, the north-star accuracy form). */
 int vp3d_stream_create(vp3d_handle* h, int dtype, vp3d_stream** out);
 /* Restart the stream (the next frame is frame 0).  Async on `stream`. */
 int vp3d_stream_reset(vp3d_stream* s, void* stream);
@@ -177,15 +186,15 @@ int64_t vp3d_stream_frames_seen(vp3d_stream* s);
 int vp3d_stream_graph_capture(vp3d_stream* s, void* stream, int steps);
 int vp3d_stream_graph_launch(vp3d_stream* s, void* stream);
 int vp3d_stream_destroy(vp3d_stream* s);
-/* 1 when the stream runs as one persistent launch per batch of steps (16-bit weights
- * resident in LDS, layer outputs handed between CUs in-launch), 0 for one GEMV launch
- * per layer (fp32 weights, or VP3D_STREAM_MODE=launches at vp3d_stream_create). */
+/* 1 when the stream runs as one persistent launch per batch of steps (weights resident
+ * on chip, layer outputs handed between CUs in-launch), 0 for one GEMV launch per layer
+ * (VP3D_STREAM_MODE=launches at vp3d_stream_create, or a shape no persistent form takes). */
 int vp3d_stream_persistent(const vp3d_stream* s);
 /* Form of the in-launch step: 2 = layer-pipelined (stream_pipe.hip: each CU runs one
  * layer with its weights in VGPRs, frames of a batch pipelined through the layer groups;
- * the default for 16-bit weights at 1024 / 256 channels with 3-tap blocks), 1 = every CU
- * runs every layer with its weights in LDS (stream_persist.hip), 0 = one GEMV launch per
- * layer.  VP3D_STREAM_MODE=pipe|persist|launches at vp3d_stream_create restricts it. */
+ * the default at 1024 / 256 channels with 3-tap blocks, f32 weights held as they are,
+ * 16-bit ones widened to f32), 1 = every CU runs every layer with its 16-bit weights in LDS
+ * (stream_persist.hip), 0 = one GEMV launch per layer.  VP3D_STREAM_MODE=pipe|persist|launches at vp3d_stream_create restricts it. */
 int vp3d_stream_mode(const vp3d_stream* s);
 /* Synchronises; VP3D_ERR_STATE if a persistent launch gave up waiting on another CU
  * (bounded spins: the grid did not fit the device at once), else VP3D_OK. */

@@ -315,6 +315,38 @@ def test_a4_split_k_last_round(dtype, monkeypatch):
     _check(y[sel], ref, gt, dtype)
 
 
+def test_a4_split_k_timeout_raises(monkeypatch):
+    """Fault injection for the split-K owner's bounded wait (conv_gemm_a4.hip owner_wait):
+    VP3D_A4_SPLIT_DROP=1 makes every helper unit skip its count, so each owner tile of the
+    partial last round (f16x3 k3 convs at 8,192 windows) gives up after its bound
+    (VP3D_A4_SPLIT_SPIN_TICKS, 1 ms here).  The fault must surface, not pass as poses:
+    the next forward on the handle is refused and sync_status raises RuntimeError; after
+    sync_status cleared it (tile flags re-zeroed) the handle reproduces the good poses bit
+    for bit."""
+    model, _ = make_model(True, (3, 3, 3, 3, 3), False, 1024)
+    B = 8192
+    x = torch.from_numpy(synth.normalized_windows(5, "x8192_243", B, 243)).cuda()
+    model.cuda().set_compute_dtype("f16x3")
+    lifter = model.native_lifter()
+    with torch.no_grad():
+        good = model(x).cpu().numpy()
+        lifter.sync_status()  # no fault on the default path
+        monkeypatch.setenv("VP3D_A4_SPLIT_DROP", "1")
+        monkeypatch.setenv("VP3D_A4_SPLIT_SPIN_TICKS", "100000")
+        model(x)
+        torch.cuda.synchronize()
+        monkeypatch.delenv("VP3D_A4_SPLIT_DROP")
+        monkeypatch.delenv("VP3D_A4_SPLIT_SPIN_TICKS")
+        with pytest.raises(RuntimeError, match="split-K"):
+            model(x)  # refused at entry: the fault of the last forward is pending
+        with pytest.raises(RuntimeError, match="split-K"):
+            lifter.sync_status()
+        lifter.sync_status()  # cleared
+        again = model(x).cpu().numpy()
+        lifter.sync_status()
+    assert np.array_equal(again, good)
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16", "f16x3"])
 @pytest.mark.parametrize("B", [8192, 300])
 def test_expand_split_round_bit_identical(dtype, B, monkeypatch):
