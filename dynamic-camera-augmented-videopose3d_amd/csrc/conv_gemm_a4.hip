@@ -437,34 +437,34 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         });
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         pinned_barrier();
-        if (tid == 0 && !p.sk_drop) __hip_atomic_fetch_add(p.sk_flag + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            const SplitCtl* ctl = (const SplitCtl*)((const char*)p.sk_flag + kSplitCtlOffset);
+            if (!ctl->drop) __hip_atomic_fetch_add(p.sk_flag + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     };
-    // the owner's helpers that delivered: S, or 1 after a timed-out wait (their partial sums
-    // are then skipped and the fault reported through sk_err, never added half-written)
-    __shared__ int s_sk_ok;
-    int sk_n = S;
+    // bounded (SplitCtl::spin_ticks); on the bound the fault goes to the host-mapped word and
+    // the epilogue runs on (its output is reported wrong by the host, vp3d_sync_status)
     auto owner_wait = [&](int si) __attribute__((always_inline)) {
         if (tid == 0) {
-            int ok = 1;
+            const SplitCtl* ctl = (const SplitCtl*)((const char*)p.sk_flag + kSplitCtlOffset);
+            const unsigned long long spin = ctl->spin_ticks;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             while (__hip_atomic_load(p.sk_flag + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > p.sk_spin) {
-                    ok = 0;
-                    if (p.sk_err) __hip_atomic_store(p.sk_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > spin) {
+                    unsigned* err = ctl->err;
+                    if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
             }
-            s_sk_ok = ok;
         }
         pinned_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        sk_n = __builtin_amdgcn_readfirstlane(s_sk_ok) ? S : 1;
     };
     // v (the accumulators of block R as two pairs) += the helpers' values of that block
     auto owner_add = [&](auto r_c, int si, f32x2 (&v)[2]) __attribute__((always_inline)) {
         constexpr int R = decltype(r_c)::value;
-        for (int q = 1; q < sk_n; ++q) {
+        for (int q = 1; q < S; ++q) {
             const f32x4 pr = *(const f32x4*)(part_ptr(si, q) + (R / 4) * 256);
             v[0] = v[0] + f32x2{pr[0], pr[1]};
             v[1] = v[1] + f32x2{pr[2], pr[3]};
@@ -988,10 +988,6 @@ static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk, bool need_ws = 
     const char* e = getenv("VP3D_A4_SPLIT");
     const int mode = e ? atoi(e) : 1;
     if (mode == 0 || (need_ws && (!q.sk_part || !q.sk_flag))) return;
-    const char* d = getenv("VP3D_A4_SPLIT_DROP");
-    q.sk_drop = d && atoi(d) != 0;
-    const char* sp = getenv("VP3D_A4_SPLIT_SPIN_TICKS");
-    q.sk_spin = sp ? strtoull(sp, nullptr, 10) : kSplitSpinTicks;
     const int ncu = a4_cus();
     if (ncu <= 0 || ncu > 256) return;  // the workspace holds one round of 256 slots
     if (mode == 1 && (nk < 64 || ntiles >= 8 * ncu)) return;

@@ -118,6 +118,10 @@ struct vp3d_handle {
     // helpers did not arrive in time; checked at the next call and by vp3d_sync_status
     unsigned* sk_err_host = nullptr;
     unsigned* sk_err_dev = nullptr;
+    // the split-K control block last written to the device (vp3d::SplitCtl: wait bound, fault
+    // word, fault injection), rewritten when the environment knobs change
+    unsigned long long sk_ctl_spin = 0;
+    int sk_ctl_drop = -1;
     // profiling
     bool profiling = false;
     uint64_t prof_mask = ~0ull;  // layers timed while profiling (bit i = layer i)

@@ -43,21 +43,27 @@ struct ConvGemmParams {
     // blocks [0, sk_full) whole, each later one as sk_split workgroups of a channel range.
     // A tile's flag counts its helpers in and the owner takes S - 1 back out (an atomic
     // subtract, so a helper arriving after a timed-out owner leaves it at 0, not above).  The
-    // owner's wait is bounded (sk_spin ticks of the 100 MHz clock); on the bound it skips the
-    // helpers' partial sums and stores 1 into sk_err (host-mapped: the next call on the handle,
-    // or vp3d_sync_status, reports it) -- wrong output is never silent.  sk_drop (fault-
-    // injection tests, VP3D_A4_SPLIT_DROP=1) makes the helpers skip their count.
+    // owner's wait is bounded (SplitCtl::spin_ticks); on the bound it stores 1 into the
+    // host-mapped SplitCtl::err (the next call on the handle, or vp3d_sync_status, reports it:
+    // the launch's output is wrong, never silently).  The control block sits in the flag area
+    // (kSplitCtlOffset), read only on those paths, so the kernel keeps no extra registers.
     float* sk_part;
     int* sk_flag;
     int sk_full, sk_split, sk_left;
-    unsigned* sk_err;
-    unsigned long long sk_spin;
-    int sk_drop;
+};
+
+// split-K control block at byte kSplitCtlOffset of the flag area (ConvGemmParams::sk_flag)
+struct SplitCtl {
+    unsigned long long spin_ticks;  // the owner's wait bound (100 MHz clock)
+    unsigned* err;                  // host-mapped fault word (device view)
+    int drop;                       // fault injection (VP3D_A4_SPLIT_DROP=1): helpers skip their count
+    int pad;
 };
 
 // bytes of the split-K workspace a handle provides (ConvGemmParams::sk_part, then the flags)
 constexpr size_t kSplitPartBytes = (size_t)256 * 256 * 1024;  // one round of 256 KiB slots
 constexpr size_t kSplitFlagBytes = 4096;
+constexpr size_t kSplitCtlOffset = kSplitFlagBytes - 32;  // flags: tiles of one round (<= 256) before it
 
 enum class Act { F32 = 0, BF16 = 1, F16 = 2 };
 

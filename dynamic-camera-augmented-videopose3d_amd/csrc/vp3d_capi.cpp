@@ -390,14 +390,27 @@ int ensure_split_ws(vp3d_handle* h, hipStream_t s) {
     return VP3D_OK;
 }
 
-// the workspace into p when a4 would split this layer (allocated then), else none
+// the workspace into p when a4 would split this layer (allocated then), else none; the
+// control block (vp3d::SplitCtl) follows VP3D_A4_SPLIT_SPIN_TICKS / VP3D_A4_SPLIT_DROP (tests)
 int attach_split_ws(vp3d_handle* h, ConvGemmParams& p, hipStream_t s) {
     if (!conv_gemm_a4_would_split(p)) return VP3D_OK;
     const int rc = ensure_split_ws(h, s);
     if (rc) return rc;
+    const char* sp = getenv("VP3D_A4_SPLIT_SPIN_TICKS");
+    const char* dr = getenv("VP3D_A4_SPLIT_DROP");
+    const unsigned long long spin = sp ? strtoull(sp, nullptr, 10) : vp3d::kSplitSpinTicks;
+    const int drop = dr && atoi(dr) != 0 ? 1 : 0;
+    if (spin != h->sk_ctl_spin || drop != h->sk_ctl_drop) {
+        static vp3d::SplitCtl ctl;  // the source of an async copy: outlives the call
+        ctl = vp3d::SplitCtl{spin, h->sk_err_dev, drop, 0};
+        HIP_TRY(hipMemcpyAsync((char*)h->sk_ws + kSplitPartBytes + vp3d::kSplitCtlOffset, &ctl, sizeof(ctl),
+                               hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        h->sk_ctl_spin = spin;
+        h->sk_ctl_drop = drop;
+    }
     p.sk_part = (float*)h->sk_ws;
     p.sk_flag = (int*)((char*)h->sk_ws + kSplitPartBytes);
-    p.sk_err = h->sk_err_dev;
     return VP3D_OK;
 }
 
@@ -778,7 +791,7 @@ int vp3d_sync_status(vp3d_handle* h, void* stream) {
     // every launch of this handle on `stream` is done: re-zero the tile flags (a timed-out
     // owner took back counts that never came) and clear the word, then report
     if (h->sk_ws) {
-        HIP_TRY(hipMemsetAsync((char*)h->sk_ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitFlagBytes, (hipStream_t)stream));
+        HIP_TRY(hipMemsetAsync((char*)h->sk_ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitCtlOffset, (hipStream_t)stream));
         HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     }
     *(volatile unsigned*)h->sk_err_host = 0u;
