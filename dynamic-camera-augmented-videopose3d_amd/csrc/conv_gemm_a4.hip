@@ -233,12 +233,18 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         const int rrow0 = lres ? res_row(p, m0) : 0;
         r_rsrc = make_rsrc((const char*)(lres ? (const CT*)p.R + (int64_t)rrow0 * p.ldr : (const CT*)p.A) - kReb,
                            0x7FFFFFFFu);
+        // lane values from a fresh laundered copy: nothing setup derives from them is computed
+        // ahead of the call and kept live across a K loop or an epilogue
+        int sln = lane, swv = widu;
+        asm volatile("" : "+v"(sln));
+        launder_s(swv);
+        const int spr = sln >> 3;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int q = GD ? 8 * wid + i : wid + 4 * i;  // the piece's slot: rows 8q .. 8q + 7
-            const int lci = GD ? (lane & 7) ^ (((i & 1) * 4 + (prow >> 1)) & 7) : lc;
+            const int q = GD ? 8 * swv + i : swv + 4 * i;  // the piece's slot: rows 8q .. 8q + 7
+            const int lci = GD ? (sln & 7) ^ (((i & 1) * 4 + (spr >> 1)) & 7) : lc;
             const int reb = GD ? kReb - (i & 3) * 1024 : 0;
-            int m = m0 + 8 * q + prow;
+            int m = m0 + 8 * q + spr;
             m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
             va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lci * 8) * (int)sizeof(CT) + reb);
             vw[i] = (uint32_t)(((8 * q + prow) * p.Kp + lci * 8) * (int)sizeof(CT) + reb);  // W rows padded
@@ -541,6 +547,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     bool first = true;
     bool prev_lres = false;  // the previous unit's epilogue took residual parts (its store order)
     bool x3_prev_res = false;  // X3: the previous unit's epilogue loaded residual rows after its DMA
+    bool x3_prev_xres = false;  // X3: ... took its residual through LDS (K-tiles 0, 1 issued before its H1 stores)
     for (;;) {
         // the per-lane constants go through an empty asm every tile: otherwise the compiler
         // hoists every address derived from them out of the tile loop and keeps them live
@@ -563,7 +570,12 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             // order); only its last stores may still be in flight.  Without one (a walked layer
             // with no residual: VP3D_A4_WALK=2; a helper unit's release fence drained anyway)
             // they may not have landed: drain.
-            if (!x3_prev_res) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // with the residual through LDS: K-tile 0 landed; younger are K-tile 1 and the previous
+            // epilogue's 32 H1 stores
+            if (x3_prev_xres)
+                asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+            else if (!x3_prev_res)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
             // younger: K-tile 1 (16 pieces) and the previous epilogue's 32 stores (with a
             // residual: the H0 stores, K-tile 1, the H1 stores)
@@ -587,8 +599,47 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             //   B1 (64 MFMAs W_hi.A_lo):  A_hi of t + 1 -> fa[1-h], row block i-1 in row block i
             //                             (its A_lo used up); 8 DMA pieces of t + 2
             //   B2 (64 MFMAs W_lo.A_hi):  W_hi of t + 1 -> fw[0] (used up in B1); 8 DMA pieces
+            // ---- the 1x1 + residual layers: the residual through LDS (round 5).  A tile's residual
+            // is 256 rows x 256 channels of [hi | lo] halves = 256 KiB: four quarters Q(hh, wc) of
+            // 64 KiB (channel half hh of wave column wc: 256 rows x 256 contiguous bytes, two groups
+            // of 32 channels, [hi | lo] each).  Q(0, 0) and Q(0, 1) land by LDS-DMA in phase B of
+            // the last two K-tiles (their own buffers, which no later K-tile needs), Q(1, *) during
+            // the half-0 epilogue; the next tile's K-tiles 0 and 1 are staged once half 1 is read.
+            // LDS image: 1 KiB slot 2q + s = rows 8q .. 8q + 7 (q = the A piece of those rows), the
+            // 128-byte group s of each row, 16-byte chunks with the A pieces' swizzle.  Per-lane
+            // source offsets vr[i] (the A pieces' rows, computed once the A / W DMA offsets are
+            // dead: the K loop has no VGPRs to spare) ----
+            const bool xres = X3 == 1 && !SPLIT && !(ABL & 40) && p.R != nullptr && role != kHelper && nk >= 3;
+            __amdgpu_buffer_rsrc_t xr_rsrc;
+            auto xres_prep = [&]() __attribute__((always_inline)) {
+                // lane values through an empty asm: nothing derived from them is hoisted out of
+                // the tile loop (the K loop has no VGPRs to spare)
+                int ln = lane, wv = widu;
+                asm volatile("" : "+v"(ln));
+                launder_s(wv);
+                const int pr = ln >> 3;
+                const int rrow0x = res_row(p, m0);
+                xr_rsrc = make_rsrc((const char*)((const f16*)p.R + (int64_t)rrow0x * p.ldr), 0x7FFFFFFFu);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    int m = m0 + 8 * (8 * wv + i) + pr;
+                    m = m < p.M ? m : p.M - 1;
+                    const int lci = (ln & 7) ^ (((i & 1) * 4 + (pr >> 1)) & 7);
+                    vr[i] = (uint32_t)((res_row(p, m) - rrow0x) * p.ldr * 2 + lci * 16);
+                }
+            };
+            // piece (i, s) of quarter (hh, wcq): this wave's A-piece rows i, 128-byte group s
+            auto xres_piece = [&](char* buf, auto i_c, auto s_c, int wcq, int hh) __attribute__((always_inline)) {
+                constexpr int I = decltype(i_c)::value;
+                constexpr int S2 = decltype(s_c)::value;
+                int w = widu;
+                launder_s(w);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(xr_rsrc, (lds_ptr_t)(buf + (2 * (8 * w + I) + S2) * 1024), 16, vr[I],
+                                                         (uint32_t)(4 * (n0 + wcq * 128 + 64 * hh) + S2 * 128), 0, 0);
+            };
             auto x3_phase = [&](auto h_c, auto kind_c, auto zero_c, auto rd_c, auto dma_c, const char* rbuf, char* dbuf,
-                                int s) __attribute__((always_inline)) {
+                                int s, auto rq_c, char* rqbuf) __attribute__((always_inline)) {
+                constexpr int RQ = decltype(rq_c)::value;  // residual quarter (0, RQ) into rqbuf, or -1
                 constexpr int H = decltype(h_c)::value;
                 constexpr int KIND = decltype(kind_c)::value;  // 0 = A, 1 = B1, 2 = B2
                 constexpr bool ZERO = decltype(zero_c)::value;
@@ -610,6 +661,8 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                             if constexpr (DO_RD && J == 0 && I > 0)
                                 fa[1 - H][I - 1] = *(const u32x4*)(rbuf + a_base + (I - 1) * 2048 + fo0);
                             if constexpr (DO_DMA && J == 4) dma_piece(dbuf, i_c, s, aoff, bs);
+                            if constexpr (RQ >= 0 && (J == 2 || J == 6))
+                                xres_piece(rqbuf, i_c, std::integral_constant<int, J / 4>{}, RQ, 0);
                             amma<CT, 4 * (8 * I + J), false>(fw[0][J], fa[1 - H][I]);
                         } else {
                             if constexpr (DO_RD && J == 0 && I == 0)
@@ -617,6 +670,8 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                             if constexpr (DO_RD && J == 4) fw[0][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo0);
                             if constexpr (DO_DMA && J == 2)
                                 dma_piece(dbuf, std::integral_constant<int, 8 + I>{}, s, aoff, bs);
+                            if constexpr (RQ >= 0 && (J == 2 || J == 6))
+                                xres_piece(rqbuf, i_c, std::integral_constant<int, J / 4>{}, RQ, 0);
                             amma<CT, 4 * (8 * I + J), false>(fw[1][J], fa[H][I]);
                         }
                         __builtin_amdgcn_sched_barrier(0);
@@ -631,18 +686,31 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             // vm: the mid wait (K-tile 0 of a walked tile: 63 = none on vmcnt -- K-tile 1 was issued
             // before the previous epilogue's residual loads, which that epilogue waited for, and
             // vmcnt retires in issue order -- so that epilogue's last stores stay in flight)
-            auto x3_ktile = [&](auto h_c, auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o, int vm = 0)
-                                __attribute__((always_inline)) {
-                x3_phase(h_c, K0{}, zero_c, T_{}, F_{}, b, nullptr, 0);
+            // rql: the last K-tile of a residual-through-LDS unit -- quarter (0, 0) into `o` (K-tile
+            // nk - 2's buffer) in phase B1, quarter (0, 1) into `b` in B2, 2 pieces per row block
+            // (both buffers are free past this K-tile's mid barrier)
+            auto x3_ktile_q = [&](auto h_c, auto zero_c, auto rd_c, auto dma_c, auto rql_c, int t, char* b, char* o,
+                                  int vm) __attribute__((always_inline)) {
+                constexpr bool rql = decltype(rql_c)::value;
+                x3_phase(h_c, K0{}, zero_c, T_{}, F_{}, b, nullptr, 0, std::integral_constant<int, -1>{}, nullptr);
                 if (vm == 63)
                     __builtin_amdgcn_s_waitcnt(kLgkm0);
+                else if (vm == 32)
+                    __builtin_amdgcn_s_waitcnt(kVm32Lgkm0);
                 else
                     __builtin_amdgcn_s_waitcnt(kVm0Lgkm0);
                 pinned_barrier();
-                x3_phase(h_c, K1{}, F_{}, rd_c, dma_c, o, b, t + 2);
-                x3_phase(h_c, K2{}, F_{}, rd_c, dma_c, o, b, t + 2);
+                x3_phase(h_c, K1{}, F_{}, rd_c, dma_c, o, b, t + 2, std::integral_constant<int, rql ? 0 : -1>{}, o);
+                x3_phase(h_c, K2{}, F_{}, rd_c, dma_c, o, b, t + 2, std::integral_constant<int, rql ? 1 : -1>{}, b);
             };
-            const int vm0 = first ? 0 : 63;
+            auto x3_ktile = [&](auto h_c, auto zero_c, auto rd_c, auto dma_c, int t, char* b, char* o, int vm = 0)
+                                __attribute__((always_inline)) {
+                x3_ktile_q(h_c, zero_c, rd_c, dma_c, std::false_type{}, t, b, o, vm);
+            };
+            // a walked tile after a residual-through-LDS epilogue: K-tile 1 landed, that
+            // epilogue's 32 H1 stores may stay in flight (32); after a global-residual one nothing
+            // on vmcnt (63); the first tile drains
+            const int vm0 = first ? 0 : (x3_prev_xres ? 32 : 63);
             if (nk > 2)
                 x3_ktile(C0{}, T_{}, T_{}, T_{}, 0, buf0, buf1, vm0);
             else if (nk == 2)
@@ -657,10 +725,20 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             if (t + 2 < nk) {
                 x3_ktile(C1{}, F_{}, T_{}, T_{}, t, buf1, buf0);
                 x3_ktile(C0{}, F_{}, T_{}, F_{}, t + 1, buf0, buf1);
-                x3_ktile(C1{}, F_{}, F_{}, F_{}, t + 2, buf1, buf0);
+                if (xres) {
+                    xres_prep();
+                    x3_ktile_q(C1{}, F_{}, F_{}, F_{}, std::true_type{}, t + 2, buf1, buf0, 0);
+                } else {
+                    x3_ktile(C1{}, F_{}, F_{}, F_{}, t + 2, buf1, buf0);
+                }
             } else if (t + 1 < nk) {
                 x3_ktile(C1{}, F_{}, T_{}, F_{}, t, buf1, buf0);
-                x3_ktile(C0{}, F_{}, F_{}, F_{}, t + 1, buf0, buf1);
+                if (xres) {
+                    xres_prep();
+                    x3_ktile_q(C0{}, F_{}, F_{}, F_{}, std::true_type{}, t + 1, buf0, buf1, 0);
+                } else {
+                    x3_ktile(C0{}, F_{}, F_{}, F_{}, t + 1, buf0, buf1);
+                }
             } else if (t < nk) {
                 x3_ktile(C1{}, F_{}, F_{}, F_{}, t, buf1, buf0);
             }
@@ -671,58 +749,53 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             // next tile's first K-tiles); em0 / en0 keep this tile's origin
             const int em0 = m0, en0 = n0;
             const int erole = role, esidx = sidx, esq = sq;
-            if (has_next) {
-                setup(next);
-                stage_01();
-            }
-            if (erole == kHelper) {
-                helper_store(esidx, esq);
-                x3_prev_res = false;
-                if (!has_next) break;
-                tix = next;
-                first = false;
-                continue;
-            }
-            if (erole == kOwner) owner_wait(esidx);
-            // split epilogue per 64 channels (the arithmetic of gemm::epilogue_tp_x3, so the same
-            // bits): BN as v_pk_mul_f32 + v_pk_add_f32, ReLU as an integer max on the f32 bits,
-            // v_permlane16_swap to 8 consecutive channels per lane, residual hi + lo added in f32,
-            // output split into hi / lo halves (16 bytes each) or f32 rows (X3 = 2).  The
-            // residual of a whole half (8 row blocks x 2 x hi / lo, 128 VGPRs) is loaded up front
-            // -- epilogue_tp_x3 loads it one row block ahead, a latency per row block
+            // residual through LDS: quarters (0, *) sit in the buffers of K-tiles nk - 2 / nk - 1
+            char* const qb0 = (nk & 1) ? buf1 : buf0;  // quarter (*, 0): K-tile nk - 2's buffer
+            char* const qb1 = (nk & 1) ? buf0 : buf1;
+            // the half's residual rows from LDS into rr (accumulator layout as the global loads)
+            auto xres_read = [&](u32x4 (&rr)[8][2][2]) __attribute__((always_inline)) {
+                int ln = lane, wv = widu;
+                asm volatile("" : "+v"(ln));
+                launder_s(wv);
+                const char* qb = (wv & 1) ? qb1 : qb0;  // wave column wc = wid & 1
+                const int swz = (((ln >> 3) & 1) * 4 + ((ln & 7) >> 1)) & 7;
+                const int g = ln >> 4;
+                const int cc = (g & 1) * 2 + (g >> 1);  // c0 / 8
+                const char* rowp = qb + (2 * ((wv >> 1) * 16 + ((ln >> 3) & 1))) * 1024 + (ln & 7) * 128;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+                        for (int hl = 0; hl < 2; ++hl)
+                            rr[i][jp][hl] = *(const u32x4*)(rowp + (4 * i + jp) * 1024 + (((hl * 4 + cc) ^ swz) << 4));
+            };
             constexpr int OB = X3 == 2 ? 4 : 2;  // output element bytes
-            const size_t y_rest = (size_t)(p.M - em0) * p.ldy * OB;
-            const __amdgpu_buffer_rsrc_t y_rsrc = make_rsrc(
-                (const char*)p.Y + (size_t)em0 * p.ldy * OB, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
             typedef float f32x2 __attribute__((ext_vector_type(2)));
             typedef int i32x2 __attribute__((ext_vector_type(2)));
-            const bool has_r = p.R != nullptr;  // (helpers left above)
-            const int rrow0 = has_r ? res_row(p, em0) : 0;
-            const __amdgpu_buffer_rsrc_t rx_rsrc =
-                make_rsrc(has_r ? (const f16*)p.R + (int64_t)rrow0 * p.ldr : (const f16*)p.A, 0x7FFFFFFFu);
-            static_for<2>([&](auto hh_c) __attribute__((always_inline)) {
+            const bool has_r = p.R != nullptr;
+            // the epilogue's lane values from a fresh laundered copy (those of the tile top would
+            // otherwise stay live across the K loop, which has no VGPRs to spare)
+            int eln = lane, ewv = widu;
+            asm volatile("" : "+v"(eln));
+            launder_s(ewv);
+            const int egrp = eln >> 4, er16 = eln & 15;
+            const int ec0 = 8 * ((egrp & 1) * 2 + (egrp >> 1));
+            const int ewr = ewv >> 1, ewc = ewv & 1;
+            // split epilogue of channel half HH (64 channels per wave) with the residual rows in rr
+            // (WITH_R) -- the arithmetic of gemm::epilogue_tp_x3, so the same bits: BN as
+            // v_pk_mul_f32 + v_pk_add_f32, ReLU as an integer max on the f32 bits,
+            // v_permlane16_swap to 8 consecutive channels per lane, residual hi + lo added in f32,
+            // output split into hi / lo halves (16 bytes each) or f32 rows (X3 = 2)
+            auto x3_half = [&](auto hh_c, auto wr_c, const u32x4 (&rr)[8][2][2], __amdgpu_buffer_rsrc_t y_rsrc)
+                               __attribute__((always_inline)) {
                 constexpr int HH = decltype(hh_c)::value;
-                const int nw = en0 + wc * 128 + 64 * HH;
-                u32x4 rres[8][2][2];  // [row block][jp][hi, lo]
-                if (has_r) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        int m = em0 + wr * 128 + 16 * i + (lane & 15);
-                        m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
-                        const int off = ((res_row(p, m) - rrow0) * p.ldr + 2 * nw + c0) * 2;
-#pragma unroll
-                        for (int jp = 0; jp < 2; ++jp) {
-                            rres[i][jp][0] = __builtin_bit_cast(
-                                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_rsrc, off + 128 * jp, 0, 0));
-                            rres[i][jp][1] = __builtin_bit_cast(
-                                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_rsrc, off + 128 * jp + 64, 0, 0));
-                        }
-                    }
-                }
+                constexpr bool WITH_R = decltype(wr_c)::value && !(ABL & 8);
+                const int nw = en0 + ewc * 128 + 64 * HH;
                 f32x2 sc[4][2], sh[4][2];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int n = nw + 16 * j + 4 * grp;
+                    const int n = nw + 16 * j + 4 * egrp;
                     const f32x4 s4 = *(const f32x4*)&s_scale[n];
                     const f32x4 h4 = *(const f32x4*)&s_shift[n];
                     sc[j][0] = f32x2{s4[0], s4[1]};
@@ -732,7 +805,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 }
                 static_for<8>([&](auto i_c) __attribute__((always_inline)) {
                     constexpr int I = decltype(i_c)::value;
-                    const int m = em0 + wr * 128 + 16 * I + (lane & 15);
+                    const int m = em0 + ewr * 128 + 16 * I + er16;
                     float v4[4][4];  // [block j][element]: BN + ReLU, accumulator layout
                     static_for<4>([&](auto j_c) __attribute__((always_inline)) {
                         constexpr int J = decltype(j_c)::value;
@@ -761,9 +834,9 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                                      : "+v"(x[0]), "+v"(y[0]), "+v"(x[1]), "+v"(y[1]), "+v"(x[2]), "+v"(y[2]),
                                        "+v"(x[3]), "+v"(y[3]));
                         float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-                        if (has_r) {
+                        if constexpr (WITH_R) {
                             // v + (rh + rl): the exact pair sums as mixed FMAs, then one f32 add each
-                            const u32x4 rh = rres[I][jp][0], rl = rres[I][jp][1];
+                            const u32x4 rh = rr[I][jp][0], rl = rr[I][jp][1];
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
                                 float t0, t1;
@@ -775,7 +848,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                         const bool in = m < p.M;
                         if constexpr (X3 == 2) {
                             const uint32_t yo =
-                                in ? (uint32_t)(((size_t)(m - em0) * p.ldy + nw + 32 * jp + c0) * 4) : 0xFFFFFFE0u;
+                                in ? (uint32_t)(((size_t)(m - em0) * p.ldy + nw + 32 * jp + ec0) * 4) : 0xFFFFFFE0u;
                             __builtin_amdgcn_raw_buffer_store_b128(
                                 __builtin_bit_cast(u32x4, f32x4{v[0], v[1], v[2], v[3]}), y_rsrc, yo, 0, 0);
                             __builtin_amdgcn_raw_buffer_store_b128(
@@ -789,15 +862,112 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                                 ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                             }
                             const uint32_t yo =
-                                in ? (uint32_t)(((size_t)(m - em0) * p.ldy + 2 * nw + 64 * jp + c0) * 2) : 0xFFFFFF00u;
-                            __builtin_amdgcn_raw_buffer_store_b128(oh, y_rsrc, yo, 0, 0);
-                            __builtin_amdgcn_raw_buffer_store_b128(ol, y_rsrc, yo + 64, 0, 0);
+                                in ? (uint32_t)(((size_t)(m - em0) * p.ldy + 2 * nw + 64 * jp + ec0) * 2) : 0xFFFFFF00u;
+                            if constexpr ((ABL & 16) != 0) {  // (measurement builds: no output stores)
+                                asm volatile("" ::"v"(oh), "v"(ol));
+                            } else {
+                                __builtin_amdgcn_raw_buffer_store_b128(oh, y_rsrc, yo, 0, 0);
+                                __builtin_amdgcn_raw_buffer_store_b128(ol, y_rsrc, yo + 64, 0, 0);
+                            }
                         }
                     }
                 });
-            });
-            if (erole == kOwner) owner_done(esidx);
+            };
+            auto y_rsrc_of = [&]() __attribute__((always_inline)) {
+                // the output resource starts at the tile's first row (outputs past 2^31 bytes)
+                const size_t y_rest = (size_t)(p.M - em0) * p.ldy * OB;
+                return make_rsrc((const char*)p.Y + (size_t)em0 * p.ldy * OB,
+                                 clamp_range31(y_rest));
+            };
+            if (xres) {
+                // ---- residual through LDS: half 0 from quarters (0, *) into registers, quarters
+                // (1, *) into the same buffers (landing under half 0's epilogue), half 1, then the
+                // next tile's K-tiles 0 and 1 (in flight under half 1's epilogue) ----
+                u32x4 rr[8][2][2];
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's quarter (0, *) pieces
+                pinned_barrier();
+                xres_read(rr);
+                __builtin_amdgcn_s_waitcnt(kLgkm0);
+                pinned_barrier();  // every wave has its half-0 rows: the buffers take quarters (1, *)
+                static_for<8>([&](auto i_c) __attribute__((always_inline)) {
+                    xres_piece(qb0, i_c, std::integral_constant<int, 0>{}, 0, 1);
+                    xres_piece(qb0, i_c, std::integral_constant<int, 1>{}, 0, 1);
+                    xres_piece(qb1, i_c, std::integral_constant<int, 0>{}, 1, 1);
+                    xres_piece(qb1, i_c, std::integral_constant<int, 1>{}, 1, 1);
+                });
+                if (erole == kOwner) owner_wait(esidx);
+                const __amdgpu_buffer_rsrc_t y_rsrc = y_rsrc_of();
+                x3_half(std::integral_constant<int, 0>{}, T_{}, rr, y_rsrc);
+                // quarters (1, *) landed (younger: the 32 H0 stores)
+                asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                pinned_barrier();
+                xres_read(rr);
+                __builtin_amdgcn_s_waitcnt(kLgkm0);
+                pinned_barrier();
+                // the next tile's K-tiles 0 and 1 ahead of the H1 stores: its first waits leave
+                // those in flight (vmcnt retires in issue order)
+                if (has_next) {
+                    setup(next);
+                    stage_01();
+                }
+                x3_half(std::integral_constant<int, 1>{}, T_{}, rr, y_rsrc);
+                if (erole == kOwner) owner_done(esidx);
+            } else {
+                // tile walk (the 1x1 + residual layers without the LDS form, VP3D_A4_WALK=2): every
+                // wave has passed the last K-tile's barrier after its last LDS reads, so both
+                // buffers take the next tile's K-tiles 0 and 1 now, ahead of this tile's epilogue
+                // loads and stores (in flight under the next tile's first K-tiles)
+                if (has_next) {
+                    setup(next);
+                    stage_01();
+                }
+                if (erole == kHelper) {
+                    helper_store(esidx, esq);
+                    x3_prev_res = false;
+                    x3_prev_xres = false;
+                    if (!has_next) break;
+                    tix = next;
+                    first = false;
+                    continue;
+                }
+                if (erole == kOwner) owner_wait(esidx);
+                const __amdgpu_buffer_rsrc_t y_rsrc = y_rsrc_of();
+                const int rrow0 = has_r ? res_row(p, em0) : 0;
+                const __amdgpu_buffer_rsrc_t rx_rsrc =
+                    make_rsrc(has_r ? (const f16*)p.R + (int64_t)rrow0 * p.ldr : (const f16*)p.A, 0x7FFFFFFFu);
+                // the residual of a whole half (8 row blocks x 2 x hi / lo, 128 VGPRs) loaded up
+                // front -- epilogue_tp_x3 loads it one row block ahead, a latency per row block
+                auto global_half = [&](auto hh_c) __attribute__((always_inline)) {
+                    constexpr int HH = decltype(hh_c)::value;
+                    const int nw = en0 + ewc * 128 + 64 * HH;
+                    u32x4 rr[8][2][2];
+                    if (has_r && !(ABL & 8)) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            int m = em0 + ewr * 128 + 16 * i + er16;
+                            m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
+                            const int off = ((res_row(p, m) - rrow0) * p.ldr + 2 * nw + ec0) * 2;
+#pragma unroll
+                            for (int jp = 0; jp < 2; ++jp) {
+                                rr[i][jp][0] = __builtin_bit_cast(
+                                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_rsrc, off + 128 * jp, 0, 0));
+                                rr[i][jp][1] = __builtin_bit_cast(
+                                    u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_rsrc, off + 128 * jp + 64, 0, 0));
+                            }
+                        }
+                        x3_half(hh_c, T_{}, rr, y_rsrc);
+                    } else {
+                        x3_half(hh_c, F_{}, rr, y_rsrc);
+                    }
+                };
+                if constexpr ((ABL & 32) == 0) {  // (measurement builds: ABL bit 5 skips the epilogue)
+                    global_half(std::integral_constant<int, 0>{});
+                    global_half(std::integral_constant<int, 1>{});
+                }
+                if (erole == kOwner) owner_done(esidx);
+            }
             x3_prev_res = has_r;
+            x3_prev_xres = xres;
             if (!has_next) break;
             tix = next;
             first = false;
@@ -873,7 +1043,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         // store offsets stay 32-bit and tile-relative; rows past M fall outside the range)
         const size_t y_rest = (size_t)(p.M - em0) * p.ldy * sizeof(CT);
         const __amdgpu_buffer_rsrc_t y_rsrc =
-            make_rsrc((const CT*)p.Y + (size_t)em0 * p.ldy, (uint32_t)(y_rest < 0x7FFFFFFFu ? y_rest : 0x7FFFFFFFu));
+            make_rsrc((const CT*)p.Y + (size_t)em0 * p.ldy, clamp_range31(y_rest));
         if (elres) {
             // residual part h into registers once landed (every wave's pieces: after the
             // barrier), then its buffer takes the next tile's K-tile h (nk even: part h sits in
@@ -1027,6 +1197,15 @@ static void a4_launch(const ConvGemmParams& p, dim3 grid, bool split, hipStream_
         hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), grid, dim3(256), 0, stream, p);
 }
 
+#ifdef VP3D_ABLATION
+// measurement builds (tools/ubench/x3_1x1_check): VP3D_ABL bits 1 no loop DMA, 2 no loop
+// fragment reads, 8 no residual loads, 16 no output stores, 32 no epilogue (timing only)
+template <int ABL>
+static void a4_x3_abl(const ConvGemmParams& p, dim3 grid) {
+    hipLaunchKernelGGL((conv_gemm_a4<_Float16, ABL, 1, true, false>), grid, dim3(256), 0, 0, p);
+}
+#endif
+
 hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p_in, bool out_f32, hipStream_t stream) {
     // the 1x1 + residual layers walk their tiles (one workgroup per CU, as launch_conv_gemm_a4);
     // VP3D_A4_WALK 0: never, 2: every layer
@@ -1040,6 +1219,25 @@ hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p_in, bool out_f32, hipS
     const int ncu = a4_cus();
     const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && nunits > ncu;
     const dim3 grid(walk ? ncu : nunits);
+#ifdef VP3D_ABLATION
+    static const int abl = [] {
+        const char* e = getenv("VP3D_ABL");
+        return e ? atoi(e) : 0;
+    }();
+    if (abl && !out_f32 && !split) {
+        switch (abl) {
+            case 1: a4_x3_abl<1>(p, grid); break;
+            case 2: a4_x3_abl<2>(p, grid); break;
+            case 3: a4_x3_abl<3>(p, grid); break;
+            case 8: a4_x3_abl<8>(p, grid); break;
+            case 16: a4_x3_abl<16>(p, grid); break;
+            case 24: a4_x3_abl<24>(p, grid); break;
+            case 32: a4_x3_abl<32>(p, grid); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+#endif
     if (out_f32)
         a4_launch<_Float16, 2>(p, grid, split, stream);
     else

@@ -262,6 +262,12 @@ __device__ __forceinline__ void epilogue_vec(const ConvGemmParams& p, const f32x
 // every wave issues exactly 2*MI stores, the count the callers' vmcnt waits use.
 // With a residual the loads run one row block ahead of the stores and are waited
 // for here (vmcnt(2)/(4): older vector-memory operations are waited for too).
+// min(bytes, 2^31 - 1) on scalar ops: a 64-bit compare against the constant becomes a VALU
+// v_cmp_lt_u64 whose constant operand the compiler keeps in a VGPR pair for the whole kernel
+__device__ __forceinline__ uint32_t clamp_range31(size_t bytes) {
+    return (bytes >> 31) != 0 ? 0x7FFFFFFFu : (uint32_t)bytes;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
