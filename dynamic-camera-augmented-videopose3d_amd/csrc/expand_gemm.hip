@@ -112,6 +112,13 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
         ch_hi = (part + 1) * nchunks / p.sk_split;
     }
     const int m_wave = rblk * kRows + wid * kRowsW;
+    // X3: this wave's output rows as a buffer resource (rows past M outside its range)
+    __amdgpu_buffer_rsrc_t y_rsrc;
+    if constexpr (X3) {
+        const int mw = __builtin_amdgcn_readfirstlane(m_wave);  // wave-uniform: an SGPR resource
+        const int64_t rows = p.M > mw ? (int64_t)(p.M - mw) : 0;
+        y_rsrc = make_rsrc((const char*)((const f16*)p.Y + (int64_t)mw * p.ldy), clamp_range31((size_t)rows * p.ldy * 2));
+    }
     u32x4* const stage = (u32x4*)(smem + RING * kChunk + wid * kRowsW * 128);
     float* const s_scale = (float*)(smem + RING * kChunk);
     float* const s_shift = s_scale + kExpMaxN;
@@ -283,6 +290,14 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                     wh[j] = *(const u32x4*)(wb + (2 * ks) * kExpSlab + j * 1024 + frag_off);
                     wl[j] = *(const u32x4*)(wb + (2 * ks + 1) * kExpSlab + j * 1024 + frag_off);
                 }
+                if (abl & 16) {  // (measurement builds: no MFMAs -- the store stream alone)
+#pragma unroll
+                    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc[rb][j] = f32x4{__builtin_bit_cast(float, wh[j][0] ^ af[rb][ks][0]), 0.f, 0.f, 0.f};
+                    continue;
+                }
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -303,7 +318,9 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
             const int n0 = ch * kExpChunkN;
             const int grp = lane >> 4;
             const int c0 = 8 * ((grp & 1) * 2 + (grp >> 1));
-            float sc[4][4], sh[4][4];
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            typedef int i32x2 __attribute__((ext_vector_type(2)));
+            f32x2 sc[4][2], sh[4][2];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 f32x4 s4, h4;
@@ -314,29 +331,44 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                     s4 = gs4[j];
                     h4 = gh4[j];
                 }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    sc[j][r] = s4[r];
-                    sh[j][r] = h4[r];
-                }
+                sc[j][0] = f32x2{s4[0], s4[1]};
+                sc[j][1] = f32x2{s4[2], s4[3]};
+                sh[j][0] = f32x2{h4[0], h4[1]};
+                sh[j][1] = f32x2{h4[2], h4[3]};
             }
+            const int r16 = lane & 15;
+            const bool top = r16 < 8;
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
                 for (int jp = 0; jp < 2; ++jp) {
-                    float v[8];
+                    // BN affine as ATen forms it (x * scale, then + shift: two roundings, packed
+                    // v_pk_mul_f32 / v_pk_add_f32) + ReLU as an integer max on the f32 bits
+                    // (negative and -0 -> +0, as x > 0 ? x : 0) in the accumulator layout (lane:
+                    // channels n0 + 16 j + 4 (l >> 4) + 0..3 of row 16 rb + (l & 15))
+                    float x[4], y[4];
 #pragma unroll
-                    for (int d = 0; d < 4; ++d) {
-                        float x = __fadd_rn(__fmul_rn(acc[rb][2 * jp][d], sc[2 * jp][d]), sh[2 * jp][d]);
-                        float y = __fadd_rn(__fmul_rn(acc[rb][2 * jp + 1][d], sc[2 * jp + 1][d]), sh[2 * jp + 1][d]);
-                        if (p.relu) {
-                            x = x > 0.f ? x : 0.f;
-                            y = y > 0.f ? y : 0.f;
+                    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+                        for (int hp = 0; hp < 2; ++hp) {
+                            const int j = 2 * jp + q;
+                            f32x2 t = f32x2{acc[rb][j][2 * hp], acc[rb][j][2 * hp + 1]} * sc[j][hp];
+                            t = t + sh[j][hp];
+                            i32x2 ti = __builtin_bit_cast(i32x2, t);  // (the X3 expand is always BN + ReLU)
+                            ti = __builtin_elementwise_max(ti, i32x2{0, 0});
+                            t = __builtin_bit_cast(f32x2, ti);
+                            float* d = q ? y : x;
+                            d[2 * hp] = t[0];
+                            d[2 * hp + 1] = t[1];
                         }
-                        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-                        v[d] = x;
-                        v[d + 4] = y;
                     }
+                    // blocks 2 jp, 2 jp + 1 -> 8 consecutive channels n0 + 32 jp + c0 + 0..7 per
+                    // lane (the x values just written by VALU: 2 wait states before the swaps)
+                    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\t"
+                                 "v_permlane16_swap_b32 %4, %5\n\tv_permlane16_swap_b32 %6, %7"
+                                 : "+v"(x[0]), "+v"(y[0]), "+v"(x[1]), "+v"(y[1]), "+v"(x[2]), "+v"(y[2]),
+                                   "+v"(x[3]), "+v"(y[3]));
+                    const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
                     // hi = f16(v), lo = f16(v - hi) (v_fma_mixlo/mixhi: one rounding each)
                     u32x4 oh, ol;
 #pragma unroll
@@ -344,10 +376,9 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                         oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
                         ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                     }
-                    const int r16 = lane & 15;
                     if constexpr (NKS > 4) {
-                        // (the camera-concat shape, one workgroup per CU: the two 64-byte halves
-                        // of 16 lines per instruction measured faster there, 7.54 vs 7.74 ms)
+                        // (the camera-concat shape: the two 64-byte halves of 16 lines per
+                        // instruction measured faster there, 7.54 vs 7.74 ms)
                         const int m = m_wave + rb * 16 + r16;
                         if (m < p.M) {
                             u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + 64 * jp + c0);
@@ -363,41 +394,33 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                     }
                     // whole 128-byte lines per store instruction: the line of row r holds its 32
                     // hi then 32 lo channels; lanes of rows 8-15 of the 16 trade with rows 0-7 (DPP
-                    // row_ror:8) so instruction A writes rows 0-7 (hi from lanes 0-7, lo from lanes
-                    // 8-15) and instruction B rows 8-15 -- instead of two 64-byte halves of 16 lines
-                    // (config 4, B = 65,536: expand 5.24-5.26 vs 5.64-5.72 ms, same box;
-                    // profiles/r04final_x3_expand_whole_lines_ab.txt)
-                    const bool top = r16 < 8;
+                    // row_ror:8, written only into the bank half that takes the partner's value)
+                    // so instruction A writes rows 0-7 (hi from lanes 0-7, lo from lanes 8-15) and
+                    // instruction B rows 8-15 -- instead of two 64-byte halves of 16 lines (config
+                    // 4, B = 65,536: 5.24-5.26 vs 5.64-5.72 ms, profiles/r04final_x3_expand_whole_lines_ab.txt)
                     u32x4 va, vb;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const uint32_t ol8 = (uint32_t)__builtin_amdgcn_mov_dpp((int)ol[e], 0x128, 0xF, 0xF, false);
-                        const uint32_t oh8 = (uint32_t)__builtin_amdgcn_mov_dpp((int)oh[e], 0x128, 0xF, 0xF, false);
-                        va[e] = top ? oh[e] : ol8;
-                        vb[e] = top ? oh8 : ol[e];
+                        va[e] = (uint32_t)__builtin_amdgcn_update_dpp((int)oh[e], (int)ol[e], 0x128, 0xF, 0xC, false);
+                        vb[e] = (uint32_t)__builtin_amdgcn_update_dpp((int)ol[e], (int)oh[e], 0x128, 0xF, 0x3, false);
                     }
-                    const int mrow = m_wave + rb * 16;
+                    if (abl & 2) {  // (measurement builds: no output stores)
+                        asm volatile("" ::"v"(va), "v"(vb));
+                        continue;
+                    }
+                    // buffer stores through the wave's own resource (rows past M fall outside it:
+                    // no exec-mask branches per store)
                     const int ra = top ? r16 : r16 - 8, rbw = top ? r16 + 8 : r16;
                     const int half = top ? 0 : 32;  // lo 64 bytes further
-                    if (mrow + ra < p.M) {
-                        u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)(mrow + ra) * p.ldy + 2 * n0 + 64 * jp + c0 + half);
-                        if constexpr (NT)
-                            __builtin_nontemporal_store(va, dst);
-                        else
-                            *dst = va;
-                    }
-                    if (mrow + rbw < p.M) {
-                        u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)(mrow + rbw) * p.ldy + 2 * n0 + 64 * jp + c0 + half);
-                        if constexpr (NT)
-                            __builtin_nontemporal_store(vb, dst);
-                        else
-                            *dst = vb;
-                    }
+                    const uint32_t oa = (uint32_t)(((rb * 16 + ra) * p.ldy + 2 * n0 + 64 * jp + c0 + half) * 2);
+                    const uint32_t ob = (uint32_t)(((rb * 16 + rbw) * p.ldy + 2 * n0 + 64 * jp + c0 + half) * 2);
+                    __builtin_amdgcn_raw_buffer_store_b128(va, y_rsrc, oa, 0, NT ? 2 : 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(vb, y_rsrc, ob, 0, NT ? 2 : 0);
                 }
             }
             asm volatile("" ::: "memory");
-            if (ch + 1 < ch_hi) {
-                if (m_wave + kRowsW > p.M)
+            if (ch + 1 < ch_hi && !(abl & 4)) {
+                if (m_wave + kRowsW > p.M || (abl & 2))
                     exp_vm<0>();
                 else if (RING == 3 && ch + 2 < ch_hi)
                     exp_vm<NKW + 4 * RB>();
@@ -595,7 +618,7 @@ hipError_t launch_expand_gemm_gather(const ConvGemmParams& p, const GatherSrc& g
 // Split-fp16 expand (X3): p.W = Layer::wx3 with p.Kp its row pitch in halves (2 Kp), the
 // scale / shift unfolded (scale_x3, shift), p.ldy the split output pitch in halves (2 N).
 bool expand_gemm_x3_eligible(const ConvGemmParams& p, const GatherSrc* g) {
-    if (p.Ktap != p.K || p.dil != 1) return false;
+    if (p.Ktap != p.K || p.dil != 1 || p.relu != 1) return false;  // expand_bn + ReLU (TemporalModel.py:127,189)
     const int nks = (p.K + 31) / 32;
     if (nks < 1 || nks > 5 || 2 * nks * 32 > p.Kp) return false;
     if (p.K % 2 || p.lda % 2 || (!g && (reinterpret_cast<uintptr_t>(p.A) & 7))) return false;

@@ -82,6 +82,38 @@ int main(int argc, char** argv) {
     g.kps = d_kps; g.f2 = F2; g.seq_off = d_off; g.seq_len = d_len; g.pairs = d_pairs; g.lead = LEAD;
     if (!expand_gather_eligible(p, g, Act::BF16, Act::BF16)) { printf("not eligible\n"); return 1; }
 
+    // VP3D_X3=1: the split-fp16 expand (random [hi | lo] weight slabs, timing only)
+    const bool x3 = getenv("VP3D_X3") != nullptr;
+    if (x3) {
+        unsigned short* d_wx;
+        unsigned short* d_yx;
+        std::vector<unsigned short> wx((size_t)N * 2 * KP);
+        for (auto& v : wx) v = (unsigned short)(((s = s * 1664525u + 1013904223u) >> 8) & 0x3BFF);
+        if (hipMalloc(&d_wx, wx.size() * 2) || hipMalloc(&d_yx, (size_t)M * N * 4)) { printf("alloc failed\n"); return 1; }
+        (void)hipMemcpy(d_wx, wx.data(), wx.size() * 2, hipMemcpyHostToDevice);
+        ConvGemmParams q = p;
+        q.W = d_wx; q.Kp = 2 * KP; q.ldy = 2 * N; q.Y = d_yx;
+        if (!expand_gemm_x3_eligible(q, &g)) { printf("x3 not eligible\n"); return 1; }
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        const int nabl = argc > 3 ? argc - 3 : 1;
+        for (int r = 0; r < 3; ++r)
+            for (int a = 0; a < nabl; ++a) {
+                const int abl = argc > 3 ? atoi(argv[3 + a]) : 0;
+                if (expand_gemm_set_ablation(abl) != hipSuccess) { printf("set ablation failed\n"); return 1; }
+                for (int i = 0; i < 2; ++i) (void)launch_expand_gemm_x3(q, &g, 0);
+                (void)hipEventRecord(e0, 0);
+                for (int i = 0; i < 10; ++i) (void)launch_expand_gemm_x3(q, &g, 0);
+                (void)hipEventRecord(e1, 0);
+                if (hipEventSynchronize(e1) != hipSuccess) { printf("launch failed\n"); return 1; }
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                ms /= 10;
+                printf("x3 round %d abl %d: %.4f ms  %.2f TB/s output\n", r, abl, ms, (double)M * N * 4 / ms / 1e9);
+            }
+        return 0;
+    }
     (void)expand_gemm_set_ablation(0);
     if (launch_expand_gemm_gather(p, g, Act::BF16, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         printf("launch failed\n");
