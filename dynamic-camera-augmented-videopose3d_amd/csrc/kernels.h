@@ -254,6 +254,13 @@ struct StreamPipeParams {
     unsigned* end_claim;
     unsigned* ended_host;                  // host-mapped copy of the end frame + 1 (0 while serving)
     unsigned long long idle_ticks;
+    // serve form, shrink folded into the last block's 1x1 (fold != 0; round 5): that role's
+    // workgroups each sum the shrink over their own channels (Nout partial sums in a fixed
+    // order, padded to 64 granules per workgroup) and store them to the host ring pose_gran
+    // [queue][n_parts x 64] instead of handing their channels to the shrink role; the host adds
+    // the n_parts partials of an output in workgroup order, then the bias.  One layer group
+    // and its all-gather fewer on a frame's path (the graph form keeps the shrink role)
+    int fold;
     // diagnostics (VP3D_STREAM_TRACE=n at vp3d_stream_create): every workgroup records the
     // 100 MHz clock when the input of its frame s < trace_frames is complete (slot 0) and, per
     // wave w, after the wave's first output store (slot 1 + w):

@@ -300,8 +300,9 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     const int nE = 2 * nb + 1;
     // per-role parameters selected with compile-time indices (a runtime index into the
     // by-value kernel argument would copy it to scratch)
-    int role = -1, gi = 0, gn = 1, N = 0, Kpr = 0, Nout = 0, K0 = 0, d = 1, R = 0;
+    int role = -1, gi = 0, gn = 1, N = 0, Kpr = 0, Nout = 0, K0 = 0, d = 1, R = 0, Kps = 0, nparts = 0;
     const void* Wr = nullptr;
+    const void* Wsh = nullptr;  // the shrink's weights (the folded last 1x1 reads its columns)
     const float* scr = nullptr;
     const float* shr = nullptr;
 #pragma unroll
@@ -316,7 +317,12 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
             scr = p.scale[l];
             shr = p.shift[l];
         }
-        if (l == nl - 1) Nout = p.N[l];
+        if (l == nl - 1) {
+            Nout = p.N[l];
+            Kps = p.Kp[l];
+            Wsh = p.W[l];
+        }
+        if (l == nl - 2) nparts = p.cu0[l + 1] - p.cu0[l];
     }
     if (role < 0) return;
     // a stream that timed out stays failed until vp3d_stream_reset: no-op launches (no
@@ -330,6 +336,11 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
     const bool is_expand = role == 0, is_shrink = role == nl - 1;
     const bool is_k = !is_expand && !is_shrink && (role & 1);
     const bool is_p = !is_expand && !is_shrink && !(role & 1);
+    // serve form only: the pipelined graph form keeps the shrink role's all-gather (the folded
+    // 1x1 stage is its slowest: 2.56 vs 2.46 us/step); serving, the fold takes a layer group
+    // and its all-gather off the frame's path (median 24.3 vs 25.2 us)
+    const bool fold_p = SERVE && p.fold && role == nl - 2;  // the last block's 1x1: shrink partials out
+    const bool fold_s = SERVE && p.fold && is_shrink;       // the shrink role: idle (the host sums)
     const int b = is_k ? (role + 1) / 2 : role / 2;  // block of a k / p role
 #pragma unroll
     for (int q = 1; q <= kStreamMaxBlocks; ++q)
@@ -357,6 +368,8 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         scl[c - c_lo] = scr[c];
         scl[kPipeMaxCh + c - c_lo] = shr[c];
     }
+    if (fold_p)  // the folded shrink's channel buffer: slots past c_hi stay zero
+        for (int i = tid; i < 64; i += kThreads) xin[i] = 0.f;
     float* gstate = p.state + (int64_t)wg * p.state_stride;
     if (is_k)
         for (int i = tid; i < kWaves * R * CWK; i += kThreads) ring[i] = gstate[i];
@@ -586,10 +599,22 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
         }
         __syncthreads();
         for (int i = tid; i < kWaves * R * CWK; i += kThreads) gstate[i] = ring[i];
+    } else if (fold_s) {
+        // ---- folded shrink, serving: the host adds the last 1x1's partial sums (nothing to do) ----
     } else {
         // ---- block b's 1x1 conv (+ residual x_b(t)) or the shrink: CWP rows per wave ----
         f2 w[1][CWP][KS / 2];
         load_rows<WT, 1, CWP, KS>(w, (const WT*)Wr, Kpr, C, c_lo, c_hi, wid, lane, 1, contig);
+        // folded shrink (the last block's 1x1): thread i sums output o = i >> 3 over the 8
+        // channels c_lo + 8 (i & 7) + k of this workgroup (shrink weights in registers)
+        const int fo = tid >> 3, fpart = tid & 7;
+        float wsh[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int c = c_lo + 8 * fpart + k;
+            wsh[k] = fold_p && fo < Nout && c < c_hi ? (float)((const WT*)Wsh)[(int64_t)fo * Kps + c] : 0.f;
+        }
+        float* ybuf = xin;  // (LDS of the expand role: unused here) this frame's channel outputs
         // after rows_sum lane l holds row l >> 3 of the wave's rows: lanes 8 j lead
         const int cr = row_of<CWP>(c_lo, wid, lane >> 3, contig);
         const bool lead = (lane & 7) == 0 && cr < c_hi;
@@ -625,7 +650,10 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                 if (is_p) {
                     y = y > 0.f ? y : 0.f;
                     y += rv[cr - c_lo];
-                    publish(out_at(role, t, cr), (unsigned)t + 1u, y);
+                    if (fold_p)
+                        ybuf[cr - c_lo] = y;
+                    else
+                        publish(out_at(role, t, cr), (unsigned)t + 1u, y);
                 } else if (SERVE) {
                     // host-mapped pose ring: the granule's tag tells the host it is there
                     const unsigned long long g = ((unsigned long long)((unsigned)t + 1u) << 32) | __float_as_uint(y);
@@ -633,6 +661,23 @@ __global__ __launch_bounds__(kThreads, 1) void stream_pipe_kernel(StreamPipePara
                                        __HIP_MEMORY_SCOPE_SYSTEM);
                 } else {
                     p.poses[(int64_t)(t & (Q - 1)) * Nout + cr] = y;
+                }
+            }
+            if (fold_p) {
+                // the workgroup's shrink partials: 8 channels per thread (FMA chain in k order),
+                // then the 8 threads of an output (lanes 8 j .. 8 j + 7) in a fixed DPP tree;
+                // outputs past Nout publish zeros (the granule slots of a workgroup are whole)
+                __syncthreads();
+                float a = 0.f;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) a = __builtin_fmaf(wsh[k], ybuf[8 * fpart + k], a);
+                a += dpp<0xB1>(a);   // xor 1
+                a += dpp<0x4E>(a);   // xor 2
+                a += dpp<0x141>(a);  // half mirror: the other quad of the 8 lanes
+                if (fpart == 0) {
+                    const int64_t slot = (int64_t)(t & (Q - 1)) * (nparts * 64) + gi * 64 + fo;
+                    const unsigned long long g = ((unsigned long long)((unsigned)t + 1u) << 32) | __float_as_uint(a);
+                    __hip_atomic_store(p.pose_gran + slot, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
             trace_mark(p, wg, s, 1, tid);

@@ -873,6 +873,11 @@ struct vp3d_stream {
     int pipe_lds = 0;
     unsigned long long* pipe_gran = nullptr;  // [queue][2nb+1][C] granules, cleared at reset
     size_t pipe_gran_bytes = 0;
+    // serving with the shrink folded into the last block's 1x1 (StreamPipeParams::fold): the
+    // host ring holds that role's partial sums, the host adds them with the shrink's scale / bias
+    bool fold = false;
+    int n_parts = 0;
+    std::vector<float> shrink_scale, shrink_shift;
     unsigned long long* pipe_trace = nullptr;  // VP3D_STREAM_TRACE diagnostics
     float* pipe_state = nullptr;
     // persistent forms: host-mapped mirror of the sticky timeout word (frames_seen[3]), read
@@ -1100,6 +1105,25 @@ bool stream_pipe_setup(vp3d_stream* st, int dtype) {
     }
     hipMemset(st->pipe_gran, 0, st->pipe_gran_bytes);
     hipMemset(st->pipe_state, 0, (size_t)g * p.state_stride * 4);
+    // serving: the shrink folded into the last block's 1x1 (VP3D_STREAM_FOLD=0 keeps the shrink
+    // role's all-gather): that role's workgroups cover <= 64 channels each (8 waves x 8 rows)
+    // and the outputs fit one 64-granule slot per workgroup
+    {
+        const int np = p.cu0[nl - 1] - p.cu0[nl - 2];
+        const char* fe = getenv("VP3D_STREAM_FOLD");
+        const bool want = !(fe && fe[0] == '0');
+        if (want && nout <= 64 && np >= 1 && np <= 64) {
+            const Layer& sl = h->layers[nl - 1];
+            st->shrink_scale.assign(nout, 0.f);
+            st->shrink_shift.assign(nout, 0.f);
+            if (hipMemcpy(st->shrink_scale.data(), sl.scale, 4 * nout, hipMemcpyDeviceToHost) == hipSuccess &&
+                hipMemcpy(st->shrink_shift.data(), sl.shift, 4 * nout, hipMemcpyDeviceToHost) == hipSuccess) {
+                st->fold = true;
+                st->n_parts = np;
+                p.fold = 1;
+            }
+        }
+    }
     p.frames = st->in_frame;
     p.queue = kQueue;
     p.poses = st->out_pose;
@@ -1359,6 +1383,11 @@ unsigned* serve_ctrl(vp3d_stream* st) { return (unsigned*)st->serve_host; }
 // {tag = frame + 1, f32 bits} granules: frame t in slot t % Q of each ring
 uint64_t* serve_frames(vp3d_stream* st) { return (uint64_t*)((char*)st->serve_host + kServeCtrlWords * 4); }
 uint64_t* serve_poses(vp3d_stream* st) { return serve_frames(st) + (size_t)kQueue * st->h->layers[0].cin; }
+// granules per frame slot of the host pose ring: the poses, or with the shrink folded the last
+// block's partial sums (n_parts x 64)
+size_t serve_pose_slot(const vp3d_stream* st) {
+    return st->fold ? (size_t)st->n_parts * 64 : (size_t)st->h->layers.back().cout;
+}
 template <typename T>
 T* dev_view(vp3d_stream* st, T* host_ptr) {
     return (T*)((char*)st->serve_dev + ((char*)host_ptr - (char*)st->serve_host));
@@ -1366,9 +1395,12 @@ T* dev_view(vp3d_stream* st, T* host_ptr) {
 // every pose granule of frame f carries its tag (the shrink workgroups store them last)
 bool serve_pose_ready(vp3d_stream* st, int64_t f) {
     const int nout = st->h->layers.back().cout;
-    const uint64_t* g = serve_poses(st) + (size_t)(f % kQueue) * nout;
-    for (int i = 0; i < nout; ++i)
-        if ((uint32_t)(__atomic_load_n(g + i, __ATOMIC_RELAXED) >> 32) != (uint32_t)(f + 1)) return false;
+    const uint64_t* g = serve_poses(st) + (size_t)(f % kQueue) * serve_pose_slot(st);
+    const int parts = st->fold ? st->n_parts : 1;
+    for (int w = 0; w < parts; ++w)
+        for (int i = 0; i < nout; ++i)
+            if ((uint32_t)(__atomic_load_n(g + (size_t)w * 64 + i, __ATOMIC_RELAXED) >> 32) != (uint32_t)(f + 1))
+                return false;
     return true;
 }
 // frames complete in order: advance the host's count of finished frames
@@ -1388,7 +1420,7 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     if (!(idle_ms > 0.0) || idle_ms > 1000.0) return fail(VP3D_ERR_ARG, "idle_ms must be in (0, 1000]");
     hipStream_t s = (hipStream_t)stream;
     const vp3d_handle* h = st->h;
-    const size_t bytes = kServeCtrlWords * 4 + (size_t)kQueue * (h->layers[0].cin + h->layers.back().cout) * 8;
+    const size_t bytes = kServeCtrlWords * 4 + (size_t)kQueue * (h->layers[0].cin + serve_pose_slot(st)) * 8;
     if (!st->serve_host) {
         HIP_TRY(hipHostMalloc(&st->serve_host, bytes, hipHostMallocMapped));
         HIP_TRY(hipHostGetDevicePointer(&st->serve_dev, st->serve_host, 0));
@@ -1451,8 +1483,22 @@ int vp3d_stream_serve_wait(vp3d_stream* st, int64_t frame_index, float* pose, do
     if (frame_index < 0 || frame_index >= st->posted) return fail(VP3D_ERR_ARG, "frame was not posted");
     if (st->posted - frame_index >= kQueue) return fail(VP3D_ERR_ARG, "frame's pose slot was reused");
     const auto t0 = std::chrono::steady_clock::now();
+    // a cursor over the frame's granules: each poll resumes at the first one not yet seen
+    // (with the shrink folded, 16 x 51 partials: re-reading those already seen every poll
+    // was host time on the frame's path)
+    const int nout_w = st->h->layers.back().cout;
+    const int parts_w = st->fold ? st->n_parts : 1;
+    const uint64_t* gw = serve_poses(st) + (size_t)(frame_index % kQueue) * serve_pose_slot(st);
+    int cw = 0, ci = 0;
     for (;;) {
-        if (serve_pose_ready(st, frame_index)) break;
+        while (cw < parts_w &&
+               (uint32_t)(__atomic_load_n(gw + (size_t)cw * 64 + ci, __ATOMIC_RELAXED) >> 32) == (uint32_t)(frame_index + 1)) {
+            if (++ci == nout_w) {
+                ci = 0;
+                ++cw;
+            }
+        }
+        if (cw == parts_w) break;
         if (*(volatile unsigned*)st->err_host) return fail(VP3D_ERR_STATE, kStreamFaultMsg);
         const unsigned ended = ((volatile unsigned*)serve_ctrl(st))[2];
         if (ended && (int64_t)ended - 1 <= frame_index) return fail(VP3D_ERR_STATE, "the serve launch ended before this frame");
@@ -1460,12 +1506,27 @@ int vp3d_stream_serve_wait(vp3d_stream* st, int64_t frame_index, float* pose, do
         if (ms > timeout_ms) return fail(VP3D_ERR_STATE, "serve wait timed out (the launch ended or is stalled)");
     }
     const int nout = st->h->layers.back().cout;
-    const uint64_t* g = serve_poses(st) + (size_t)(frame_index % kQueue) * nout;
-    if (pose)
-        for (int i = 0; i < nout; ++i) {
-            const uint32_t bits = (uint32_t)__atomic_load_n(g + i, __ATOMIC_RELAXED);
-            std::memcpy(pose + i, &bits, 4);
+    const uint64_t* g = serve_poses(st) + (size_t)(frame_index % kQueue) * serve_pose_slot(st);
+    auto val = [&](size_t i) {
+        const uint32_t bits = (uint32_t)__atomic_load_n(g + i, __ATOMIC_RELAXED);
+        float v;
+        std::memcpy(&v, &bits, 4);
+        return v;
+    };
+    if (pose) {
+        if (st->fold) {
+            // the shrink role's sum (stream_pipe.hip): partials in workgroup order, then the
+            // affine -- the same f32 operations, so the same bits as the graph form
+            for (int i = 0; i < nout; ++i) {
+                float a = val(i);
+                for (int w = 1; w < st->n_parts; ++w) a += val((size_t)w * 64 + i);
+                const float sa = a * st->shrink_scale[i];
+                pose[i] = sa + st->shrink_shift[i];
+            }
+        } else {
+            for (int i = 0; i < nout; ++i) pose[i] = val(i);
         }
+    }
     return VP3D_OK;
 }
 
