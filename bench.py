@@ -833,25 +833,34 @@ class WindowsCase:
             xs = self.pool.seqs.gather(self.pairs[idx].contiguous(), self.RF, self.pad, "2d",
                                        concat_cams=self.traj).view(P, self.RF, self.jin, 2)
             ref = lifter_forward(self.sd, xs.cpu(), FW, strided=True).numpy()
+            # the same windows in float64: the yardstick for how much of a delta is the
+            # reference's own fp32 rounding
+            ref64 = lifter_forward(self.sd, xs.cpu(), FW, strided=True, dtype=torch.float64).numpy()
             gt = synth.gt_poses(3, "bench_gt", P, JOINTS).reshape(ref.shape)
-            self._ref = (idx, ref, gt)
+            self._ref = (idx, ref, gt, ref64)
         return self._ref
 
-    def parity(self, y, P):
-        idx, ref, gt = self.parity_ref(P)
-        yf = y[idx].cpu().numpy()
+    @staticmethod
+    def _mp(a, gt):
+        return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
 
-        def mp(a):
-            return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
-        return {"mpjpe_delta_mm": abs(mp(yf) - mp(ref)) * 1e3,
+    def parity(self, y, P):
+        idx, ref, gt, ref64 = self.parity_ref(P)
+        yf = y[idx].cpu().numpy()
+        mp = self._mp
+        return {"mpjpe_delta_mm": abs(mp(yf, gt) - mp(ref, gt)) * 1e3,
                 "max_coord_delta_mm": float(np.abs(yf - ref).max()) * 1e3,
-                "meets_north_star_1e-4mm": bool(abs(mp(yf) - mp(ref)) * 1e3 <= 1e-4)}
+                "mpjpe_delta_vs_fp64_mm": abs(mp(yf, gt) - mp(ref64, gt)) * 1e3,
+                "meets_north_star_1e-4mm": bool(abs(mp(yf, gt) - mp(ref, gt)) * 1e3 <= 1e-4)}
 
     def parity_info(self, P):
-        idx, ref, gt = self.parity_ref(P)
+        idx, ref, gt, ref64 = self.parity_ref(P)
+        mp = self._mp
         return {"windows": int(idx.numel()), "windows_checked": "first and last half of rank 0's shard "
                 "(the timed kernels' own output)",
-                "mpjpe_ref_mm": round(float(np.mean(np.linalg.norm(ref.astype(np.float64) - gt, axis=-1))) * 1e3, 6),
+                "mpjpe_ref_mm": round(mp(ref, gt) * 1e3, 6),
+                "reference_fp32_vs_fp64_mpjpe_delta_mm": abs(mp(ref, gt) - mp(ref64, gt)) * 1e3,
+                "reference_fp32_vs_fp64_max_coord_delta_mm": float(np.abs(ref - ref64).max()) * 1e3,
                 "output_rms_m": round(float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))), 6)}
 
     def cpu_baseline(self, seconds):

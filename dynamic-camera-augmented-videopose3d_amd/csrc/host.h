@@ -114,8 +114,8 @@ struct vp3d_handle {
     // first forward whose plan splits a layer; flags zeroed then, each owner unit takes its
     // helpers' counts back out (and vp3d_sync_status re-zeroes them after a reported timeout)
     void* sk_ws = nullptr;
-    // host-mapped split-K fault word (ConvGemmParams::sk_err): set by an owner unit whose
-    // helpers did not arrive in time; checked at the next call and by vp3d_sync_status
+    // host-mapped fault word (vp3d::kFault* bits): a split-K owner unit whose helpers did not
+    // arrive in time, a non-finite f16x3 output; checked at the next call and by vp3d_sync_status
     unsigned* sk_err_host = nullptr;
     unsigned* sk_err_dev = nullptr;
     // the split-K control block last written to the device (vp3d::SplitCtl: wait bound, fault

@@ -301,6 +301,11 @@ hipError_t launch_mpjpe_backward(const float* pred, const float* target, int64_t
 hipError_t launch_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_cam, const float* params,
                                 bool linear, float* out, hipStream_t s);
 // metrics.hip: MPJPE / P-MPJPE / N-MPJPE / MPJVE partial sums per (n_frames, J, 3) pair
+// non-finite values in y[0, n) -> `bit` ORed into *flag (host-mapped fault word)
+hipError_t launch_nonfinite_check(const float* y, int64_t n, unsigned* flag, unsigned bit, hipStream_t s);
+// the handle's fault-word bits (vp3d_sync_status)
+constexpr unsigned kFaultSplitTimeout = 1u;   // a split-K owner gave up waiting for its helpers
+constexpr unsigned kFaultNonFinite = 2u;      // an f16x3 forward produced a non-finite pose value
 hipError_t launch_pose_metrics(const float* pred, const float* target, int64_t n_frames, int J, double* acc,
                                hipStream_t s);
 

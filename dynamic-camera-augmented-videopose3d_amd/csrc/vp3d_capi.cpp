@@ -372,13 +372,17 @@ const char* x3_requirement() { return "dtype f16x3 needs channels % 64 == 0 and 
 
 // The split-K workspace (kSplitPartBytes of partial sums + the tile flags) and the host-mapped
 // fault word, on the first layer whose a4 plan splits (not on every handle)
+int ensure_fault_word(vp3d_handle* h) {
+    if (h->sk_err_host) return VP3D_OK;
+    HIP_TRY(hipHostMalloc((void**)&h->sk_err_host, 4, hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->sk_err_dev, h->sk_err_host, 0));
+    *(volatile unsigned*)h->sk_err_host = 0u;
+    return VP3D_OK;
+}
+
 int ensure_split_ws(vp3d_handle* h, hipStream_t s) {
     if (h->sk_ws) return VP3D_OK;
-    if (!h->sk_err_host) {
-        HIP_TRY(hipHostMalloc((void**)&h->sk_err_host, 4, hipHostMallocMapped));
-        HIP_TRY(hipHostGetDevicePointer((void**)&h->sk_err_dev, h->sk_err_host, 0));
-        *(volatile unsigned*)h->sk_err_host = 0u;
-    }
+    if (const int rc = ensure_fault_word(h)) return rc;
     void* ws = nullptr;
     HIP_TRY(hipMalloc(&ws, vp3d::kSplitPartBytes + vp3d::kSplitFlagBytes));
     const hipError_t e = hipMemsetAsync((char*)ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitFlagBytes, s);
@@ -417,6 +421,11 @@ int attach_split_ws(vp3d_handle* h, ConvGemmParams& p, hipStream_t s) {
 constexpr const char* kSplitFaultMsg =
     "split-K: an owner tile timed out waiting for its helper units (an earlier forward on this "
     "handle produced wrong poses); vp3d_sync_status clears the fault";
+constexpr const char* kNonFiniteMsg =
+    "f16x3: an earlier forward on this handle produced non-finite poses (an activation past the "
+    "f16 range |x| < 65504 of the split halves); run those inputs in fp32. vp3d_sync_status "
+    "clears the fault";
+const char* fault_msg(unsigned w) { return (w & vp3d::kFaultSplitTimeout) ? kSplitFaultMsg : kNonFiniteMsg; }
 
 hipEvent_t get_event(vp3d_handle* h) {
     if (!h->free_events.empty()) {
@@ -461,6 +470,11 @@ int vp3d_create(const vp3d_cfg* cfg, const float* const* weights, int n_weights,
     h->prof_ms.assign(h->layers.size(), 0.0);
     h->prof_n.assign(h->layers.size(), 0);
     h->prof_flop.assign(h->layers.size(), 0.0);
+    rc = ensure_fault_word(h);  // the device fault word (vp3d_sync_status), host-mapped
+    if (rc) {
+        vp3d_destroy(h);
+        return rc;
+    }
     *out = h;
     return VP3D_OK;
 }
@@ -547,7 +561,8 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
                                       std::to_string(vp3d_receptive_field(h)));
     // a split-K timeout of an earlier launch on this handle (no synchronisation: the word is
     // host-mapped); sticky until vp3d_sync_status
-    if (h->sk_err_host && *(volatile unsigned*)h->sk_err_host) return fail(VP3D_ERR_STATE, kSplitFaultMsg);
+    if (h->sk_err_host && *(volatile unsigned*)h->sk_err_host)
+        return fail(VP3D_ERR_STATE, fault_msg(*(volatile unsigned*)h->sk_err_host));
     int rc = ensure_ws(h, B, T, dtype);
     if (rc) return rc;
 
@@ -747,6 +762,14 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         cur_len = len[li];
         (void)xin_buf;
     }
+    if (x3) {
+        // f16x3 carries every activation as f16 halves: one past |x| < 65,504 turns into inf /
+        // NaN downstream -- flagged here (one read of the poses), reported by the next call
+        if ((rc = ensure_fault_word(h))) return rc;
+        const hipError_t e = launch_nonfinite_check(y, (int64_t)B * len.back() * h->layers.back().cout,
+                                                    h->sk_err_dev, vp3d::kFaultNonFinite, s);
+        if (e != hipSuccess) return fail(VP3D_ERR_HIP, std::string("finite check: ") + hipGetErrorString(e));
+    }
     return VP3D_OK;
 }
 
@@ -790,12 +813,13 @@ int vp3d_sync_status(vp3d_handle* h, void* stream) {
     if (!h->sk_err_host || !*(volatile unsigned*)h->sk_err_host) return VP3D_OK;
     // every launch of this handle on `stream` is done: re-zero the tile flags (a timed-out
     // owner took back counts that never came) and clear the word, then report
-    if (h->sk_ws) {
+    const unsigned w = *(volatile unsigned*)h->sk_err_host;
+    if (h->sk_ws && (w & vp3d::kFaultSplitTimeout)) {
         HIP_TRY(hipMemsetAsync((char*)h->sk_ws + vp3d::kSplitPartBytes, 0, vp3d::kSplitCtlOffset, (hipStream_t)stream));
         HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     }
     *(volatile unsigned*)h->sk_err_host = 0u;
-    return fail(VP3D_ERR_STATE, kSplitFaultMsg);
+    return fail(VP3D_ERR_STATE, fault_msg(w));
 }
 
 int vp3d_profile_enable(vp3d_handle* h, int enable) {

@@ -347,6 +347,31 @@ def test_a4_split_k_timeout_raises(monkeypatch):
     assert np.array_equal(again, good)
 
 
+def test_f16x3_nonfinite_output_raises():
+    """f16x3 carries activations as f16 halves (|x| < 65,504): inputs that push one past
+    that range give inf / NaN poses.  The forward flags it on the device (a pass over the
+    poses into the handle's fault word): sync_status raises RuntimeError naming f16x3, the
+    next forward is refused until then, and the handle works again afterwards."""
+    model, _ = make_model(True, (3, 3, 3, 3, 3), False, 1024)
+    x = torch.from_numpy(synth.normalized_windows(5, "x64_243", 64, 243)).cuda()
+    model.cuda().set_compute_dtype("f16x3")
+    lifter = model.native_lifter()
+    with torch.no_grad():
+        good = model(x).cpu().numpy()
+        lifter.sync_status()
+        y = model(x * 1e6)
+        torch.cuda.synchronize()
+        assert not torch.isfinite(y).all()
+        with pytest.raises(RuntimeError, match="f16x3"):
+            model(x)
+        with pytest.raises(RuntimeError, match="non-finite"):
+            lifter.sync_status()
+        lifter.sync_status()
+        again = model(x).cpu().numpy()
+        lifter.sync_status()
+    assert np.array_equal(again, good)
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16", "f16x3"])
 @pytest.mark.parametrize("B", [8192, 300])
 def test_expand_split_round_bit_identical(dtype, B, monkeypatch):
