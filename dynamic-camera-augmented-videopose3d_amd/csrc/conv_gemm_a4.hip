@@ -856,11 +856,16 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                         } else {
                             // hi = f16(v), lo = f16(v - hi) (v_fma_mixlo/mixhi: one rounding, as before)
                             u32x4 oh, ol;
+                            float t = 0.f;
 #pragma unroll
                             for (int e = 0; e < 4; ++e) {
                                 oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
                                 ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
+                                t = gemm::x3_absmax2(t, v[2 * e], v[2 * e + 1]);
                             }
+                            // (per 8 values: a running max over the half costs a VGPR the K
+                            // loop does not have)
+                            gemm::x3_range_flag(in ? t : 0.f, p.scale, p.N);
                             const uint32_t yo =
                                 in ? (uint32_t)(((size_t)(m - em0) * p.ldy + 2 * nw + 64 * jp + ec0) * 2) : 0xFFFFFF00u;
                             if constexpr ((ABL & 16) != 0) {  // (measurement builds: no output stores)

@@ -149,6 +149,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     u32x4 af[RB][NKS];
     u32x4 afl[X3 ? RB : 1][NKS];  // X3: the lo fragments
     constexpr float kBias = X3 ? 0.f : 1.f;  // the folded-shift column (16-bit path only)
+    bool x_ok = true;  // X3: every input value within the f16 range (NaN: false)
     auto put = [&](int rb, int ks, const float (&v)[8]) {
         if constexpr (X3) {
             f16x8 h, l;
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
             for (int e = 0; e < 8; ++e) {
                 h[e] = (f16)v[e];
                 l[e] = (f16)(v[e] - (float)h[e]);
+                x_ok = x_ok && __builtin_fabsf(v[e]) <= 65504.f;
             }
             af[rb][ks] = __builtin_bit_cast(u32x4, h);
             afl[rb][ks] = __builtin_bit_cast(u32x4, l);
@@ -252,6 +254,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     }
     exp_vm<0>();  // weight chunks 0 and 1 (and the A loads) landed
     __builtin_amdgcn_s_barrier();
+    if constexpr (X3) gemm::x3_range_flag(x_ok ? 0.f : __builtin_inff(), p.scale, p.N);
 
 #ifdef VP3D_ABLATION
     // measurement builds only (tools/ubench/expand_check): 2 = no global stores,
@@ -338,6 +341,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
             }
             const int r16 = lane & 15;
             const bool top = r16 < 8;
+            float vmax = 0.f;  // |x| over what this chunk splits (gemm::x3_range_flag)
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
@@ -375,6 +379,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                     for (int e = 0; e < 4; ++e) {
                         oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
                         ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
+                        vmax = gemm::x3_absmax2(vmax, v[2 * e], v[2 * e + 1]);
                     }
                     if constexpr (NKS > 4) {
                         // (the camera-concat shape: the two 64-byte halves of 16 lines per
@@ -418,6 +423,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                     __builtin_amdgcn_raw_buffer_store_b128(vb, y_rsrc, ob, 0, NT ? 2 : 0);
                 }
             }
+            gemm::x3_range_flag(vmax, p.scale, p.N);
             asm volatile("" ::: "memory");
             if (ch + 1 < ch_hi && !(abl & 4)) {
                 if (m_wave + kRowsW > p.M || (abl & 2))

@@ -487,6 +487,22 @@ __device__ __forceinline__ uint32_t x3_hi2(float x0, float x1) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2_{x0, x1}, h2_));
 }
 
+// f16x3 range guard.  A value split into f16 halves must satisfy |x| <= 65,504: past it hi =
+// inf and every later product is inf / NaN (or, through the integer-max ReLU, silently 0).
+// The split epilogues fold |x| of what they split into a running max (x3_absmax2: one
+// v_max3_f32 per pair); at the end of a tile a lane over the range ORs kFaultNonFinite into
+// the handle's fault word, whose device address the host keeps just past the layer's
+// scale_x3 vector (Layer::scale_x3[N .. N + 1], vp3d_capi.cpp upload_weights).
+__device__ __forceinline__ float x3_absmax2(float m, float a, float b) {
+    return __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(a), __builtin_fabsf(b)));
+}
+__device__ __forceinline__ void x3_range_flag(float m, const float* scale_x3, int n) {
+    if (__builtin_expect(!(m <= 65504.f), 0)) {  // (a NaN input compares false too)
+        unsigned* const f = *(unsigned* const*)(scale_x3 + n);
+        if (f) __hip_atomic_fetch_or(f, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 template <bool OUT_F32, int HAS_R>
 __device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&acc)[8][4], int mw, int nw, int lane,
                                                const float* s_scale, const float* s_shift,
@@ -518,6 +534,7 @@ __device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&
         }
     };
     if (HAS_R) load_res(0, res[0]);
+    float vmax = 0.f;  // |x| over what this tile splits (x3_range_flag)
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
         const int m = mw + i * 16 + (lane & 15);
@@ -571,6 +588,7 @@ __device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&
                 for (int e = 0; e < 4; ++e) {
                     oh[e] = gemm::x3_hi2(v[2 * e], v[2 * e + 1]);
                     ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
+                    if (in) vmax = x3_absmax2(vmax, v[2 * e], v[2 * e + 1]);
                 }
                 const uint32_t yo = in ? (uint32_t)(((size_t)(m - m_base) * p.ldy + 2 * nw + 64 * jp + c0) * 2)
                                        : 0xFFFFFF00u;
@@ -579,6 +597,7 @@ __device__ __forceinline__ void epilogue_tp_x3(const ConvGemmParams& p, f32x4 (&
             }
         }
     }
+    if constexpr (!OUT_F32) x3_range_flag(vmax, p.scale, p.N);
 }
 
 }  // namespace gemm

@@ -293,7 +293,7 @@ hipError_t launch_pack_rows(const float* x, int M, int T_out, int T_in, int stri
 // the sequences of `g` when x is null), zero padded to Kp and stored as 2 Kp halves
 // (32-wide groups [hi | lo]).
 hipError_t launch_pack_rows_x3(const float* x, const struct GatherSrc* g, int M, int T_out, int T_in, int stride,
-                               int cin, int K, int Kp, void* out, hipStream_t s);
+                               int cin, int K, int Kp, void* out, unsigned* fault, hipStream_t s);
 hipError_t launch_mpjpe_accumulate(const float* pred, const float* target, int64_t n,
                                    double* acc, hipStream_t s);
 hipError_t launch_mpjpe_backward(const float* pred, const float* target, int64_t n, const float* grad_loss,
@@ -305,7 +305,9 @@ hipError_t launch_project_to_2d(const float* X, int64_t n_cams, int64_t pts_per_
 hipError_t launch_nonfinite_check(const float* y, int64_t n, unsigned* flag, unsigned bit, hipStream_t s);
 // the handle's fault-word bits (vp3d_sync_status)
 constexpr unsigned kFaultSplitTimeout = 1u;   // a split-K owner gave up waiting for its helpers
-constexpr unsigned kFaultNonFinite = 2u;      // an f16x3 forward produced a non-finite pose value
+// an f16x3 forward split a value past the f16 range (|x| > 65,504, gemm::x3_range_flag) or
+// produced a non-finite pose value
+constexpr unsigned kFaultNonFinite = 2u;
 hipError_t launch_pose_metrics(const float* pred, const float* target, int64_t n_frames, int J, double* acc,
                                hipStream_t s);
 

@@ -324,8 +324,9 @@ __global__ void pack_rows_x3_kernel(const float* __restrict__ x, const float* __
                                     const float* __restrict__ cams, const int64_t* __restrict__ seq_off,
                                     const int32_t* __restrict__ seq_len, const int32_t* __restrict__ pairs,
                                     int lead, int M, int T_out, int T_in, int stride, int cin, int K, int Kp,
-                                    _Float16* __restrict__ out) {
+                                    _Float16* __restrict__ out, unsigned* fault) {
     const int chunks = Kp >> 3;
+    bool ok = true;  // every value within the f16 range (NaN: false), else kFaultNonFinite
     const int64_t total = (int64_t)M * chunks;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -362,26 +363,28 @@ __global__ void pack_rows_x3_kernel(const float* __restrict__ x, const float* __
         for (int e = 0; e < 8; ++e) {
             hi[e] = (_Float16)v[e];
             lo[e] = (_Float16)(v[e] - (float)hi[e]);
+            ok = ok && __builtin_fabsf(v[e]) <= 65504.f;
         }
         _Float16* o = out + (int64_t)m * 2 * Kp + (c >> 5) * 64 + (c & 31);
         *(h8*)o = hi;
         *(h8*)(o + 32) = lo;
     }
+    if (!ok && fault) __hip_atomic_fetch_or(fault, kFaultNonFinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
 
 hipError_t launch_pack_rows_x3(const float* x, const GatherSrc* g, int M, int T_out, int T_in, int stride,
-                               int cin, int K, int Kp, void* out, hipStream_t s) {
+                               int cin, int K, int Kp, void* out, unsigned* fault, hipStream_t s) {
     if (M <= 0) return hipSuccess;
     const dim3 grid = grid_for((int64_t)M * (Kp / 8), 4);
     if (g)
         hipLaunchKernelGGL(pack_rows_x3_kernel, grid, dim3(kThreads), 0, s, nullptr, g->kps, g->f2, g->cams,
                            g->seq_off, g->seq_len, g->pairs, g->lead, M, T_out, T_in, stride, cin, K, Kp,
-                           (_Float16*)out);
+                           (_Float16*)out, fault);
     else
         hipLaunchKernelGGL(pack_rows_x3_kernel, grid, dim3(kThreads), 0, s, x, nullptr, 0, nullptr, nullptr,
-                           nullptr, nullptr, 0, M, T_out, T_in, stride, cin, K, Kp, (_Float16*)out);
+                           nullptr, nullptr, 0, M, T_out, T_in, stride, cin, K, Kp, (_Float16*)out, fault);
     return hipGetLastError();
 }
 

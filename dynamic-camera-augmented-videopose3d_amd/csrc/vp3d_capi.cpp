@@ -282,14 +282,19 @@ int upload_weights(vp3d_handle* h, const float* const* w, int n) {
                     px3[q] = hi;
                     px3[q + 32] = f32_to_f16_rne(v - f16_to_f32(hi));
                 }
-            std::vector<float> scx3(L.cout);
+            // [cout scales | the fault word's device address] (gemm::x3_range_flag; the kernels
+            // run with cout % 64 == 0, so the address is 8-byte aligned at index cout)
+            const int tail = (L.cout + 1) & ~1;
+            std::vector<float> scx3(tail + 2, 0.f);
             for (int o = 0; o < L.cout; ++o) scx3[o] = std::ldexp(balance && (o & 1) ? -sc[o] : sc[o], -e);
+            static_assert(sizeof(unsigned*) == 2 * sizeof(float), "pointer = two floats");
+            std::memcpy(&scx3[tail], &h->sk_err_dev, sizeof(unsigned*));
             if (!L.wx3) {
                 HIP_TRY(hipMalloc(&L.wx3, px3.size() * 2));
-                HIP_TRY(hipMalloc(&L.scale_x3, L.cout * 4));
+                HIP_TRY(hipMalloc(&L.scale_x3, scx3.size() * 4));
             }
             HIP_TRY(hipMemcpy(L.wx3, px3.data(), px3.size() * 2, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(L.scale_x3, scx3.data(), L.cout * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(L.scale_x3, scx3.data(), scx3.size() * 4, hipMemcpyHostToDevice));
         }
     }
     return VP3D_OK;
@@ -422,9 +427,9 @@ constexpr const char* kSplitFaultMsg =
     "split-K: an owner tile timed out waiting for its helper units (an earlier forward on this "
     "handle produced wrong poses); vp3d_sync_status clears the fault";
 constexpr const char* kNonFiniteMsg =
-    "f16x3: an earlier forward on this handle produced non-finite poses (an activation past the "
-    "f16 range |x| < 65504 of the split halves); run those inputs in fp32. vp3d_sync_status "
-    "clears the fault";
+    "f16x3: an earlier forward on this handle split an activation past the f16 range (|x| <= "
+    "65504) or produced non-finite poses; its outputs are not valid -- run those inputs in fp32. "
+    "vp3d_sync_status clears the fault";
 const char* fault_msg(unsigned w) { return (w & vp3d::kFaultSplitTimeout) ? kSplitFaultMsg : kNonFiniteMsg; }
 
 hipEvent_t get_event(vp3d_handle* h) {
@@ -461,20 +466,17 @@ int vp3d_create(const vp3d_cfg* cfg, const float* const* weights, int n_weights,
     if (h->cfg.bn_eps <= 0.f) h->cfg.bn_eps = 1e-5f;
     hipGetDevice(&h->device);
     build_geometry(h);
-    rc = upload_weights(h, weights, n_weights);
+    // the device fault word (vp3d_sync_status), host-mapped; before the weights: the f16x3
+    // layers keep its address after their scale_x3 vectors
+    rc = ensure_fault_word(h);
+    if (!rc) rc = upload_weights(h, weights, n_weights);
     if (rc) {
-        free_layers(h);
-        delete h;
+        vp3d_destroy(h);
         return rc;
     }
     h->prof_ms.assign(h->layers.size(), 0.0);
     h->prof_n.assign(h->layers.size(), 0);
     h->prof_flop.assign(h->layers.size(), 0.0);
-    rc = ensure_fault_word(h);  // the device fault word (vp3d_sync_status), host-mapped
-    if (rc) {
-        vp3d_destroy(h);
-        return rc;
-    }
     *out = h;
     return VP3D_OK;
 }
@@ -664,7 +666,7 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
                 // the expand conv's rows (window gather + camera concat fused) packed as halves
                 void* packed = base + 3 * buf_elems * es;
                 e = launch_pack_rows_x3(gs ? nullptr : x, gs, p.M, p.T_out, p.T_in, p.stride, L.cin, L.K, L.Kp,
-                                        packed, s);
+                                        packed, h->sk_err_dev, s);
                 if (e != hipSuccess) return fail(VP3D_ERR_HIP, std::string("pack: ") + hipGetErrorString(e));
                 p.A = packed;
                 p.T_in = p.T_out;

@@ -120,9 +120,9 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
 /* Synchronise `stream` and report a device-side fault of this handle's launches since the
  * last call: VP3D_ERR_STATE when a split-K owner tile (conv_gemm_a4, the partial last round
  * of small f16x3 batches) gave up waiting for its helper units -- its output was then
- * wrong -- or when an f16x3 forward produced non-finite poses (an activation past the f16
- * range of its split halves, |x| >= 65,504: run such inputs in fp32); the fault is cleared
- * by this call.  (The next vp3d_forward* on the handle also
+ * wrong -- or when an f16x3 forward split a value past the f16 range of its halves
+ * (|x| > 65,504: checked where the input rows and every hidden activation are split) or
+ * produced non-finite poses (run such inputs in fp32); the fault is cleared by this call.  (The next vp3d_forward* on the handle also
  * refuses with VP3D_ERR_STATE while the fault is pending, without synchronising.)  No
  * reference counterpart: torch raises asynchronous device errors at the next sync. */
 int vp3d_sync_status(vp3d_handle* h, void* stream);

@@ -347,28 +347,38 @@ def test_a4_split_k_timeout_raises(monkeypatch):
     assert np.array_equal(again, good)
 
 
-def test_f16x3_nonfinite_output_raises():
-    """f16x3 carries activations as f16 halves (|x| < 65,504): inputs that push one past
-    that range give inf / NaN poses.  The forward flags it on the device (a pass over the
-    poses into the handle's fault word): sync_status raises RuntimeError naming f16x3, the
-    next forward is refused until then, and the handle works again afterwards."""
+@pytest.mark.parametrize("where,B", [("input", 64), ("block0_k", 64), ("block1_1x1", 64), ("block1_1x1", 2048)])
+def test_f16x3_range_fault_raises(where, B):
+    """f16x3 carries activations as f16 halves (|x| <= 65,504).  A value past that range --
+    in the input rows (x 1e6) or in a hidden layer's output (its BN gamma x 1e6) -- is
+    flagged where it is split (gemm::x3_range_flag: the expand's input and epilogue, the q64
+    and a4 epilogues) into the handle's fault word: the next forward is refused naming
+    f16x3, sync_status raises it once, and the handle works again afterwards.  B = 64
+    windows runs the hidden layers on q64, B = 2,048 on the one-wave-per-SIMD a4 kernel."""
     model, _ = make_model(True, (3, 3, 3, 3, 3), False, 1024)
-    x = torch.from_numpy(synth.normalized_windows(5, "x64_243", 64, 243)).cuda()
+    x = torch.from_numpy(synth.normalized_windows(5, "x64_243", B, 243)).cuda()
     model.cuda().set_compute_dtype("f16x3")
     lifter = model.native_lifter()
     with torch.no_grad():
         good = model(x).cpu().numpy()
         lifter.sync_status()
-        y = model(x * 1e6)
+        if where == "input":
+            model(x * 1e6)
+        else:
+            bn = model.layers_bn[0 if where == "block0_k" else 3]
+            g0 = bn.weight.detach().clone()
+            bn.weight.mul_(1e6)
+            model(x)
+            torch.cuda.synchronize()
+            bn.weight.copy_(g0)
         torch.cuda.synchronize()
-        assert not torch.isfinite(y).all()
         with pytest.raises(RuntimeError, match="f16x3"):
             model(x)
         with pytest.raises(RuntimeError, match="non-finite"):
             lifter.sync_status()
         lifter.sync_status()
         again = model(x).cpu().numpy()
-        lifter.sync_status()
+        model.native_lifter().sync_status()
     assert np.array_equal(again, good)
 
 
