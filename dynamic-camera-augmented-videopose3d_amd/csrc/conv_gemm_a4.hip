@@ -92,6 +92,27 @@ __device__ __forceinline__ void amma(const u32x4& w, const u32x4& a) {
     }
 }
 
+#ifdef VP3D_ABLATION
+// measurement builds (ABL bit 6): a[R..R+15] (+)= one v_mfma_f32_32x32x16 on the same fragment
+// registers -- the issue pattern of a 32 x 32 block K loop (results wrong; timing only)
+template <typename CT, int R, bool ZERO>
+__device__ __forceinline__ void amma32(const u32x4& w, const u32x4& a) {
+    if constexpr (std::is_same<CT, __bf16>::value) {
+        if constexpr (ZERO)
+            asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, 0" ::"v"(w), "v"(a), "i"(R), "i"(R + 15));
+        else
+            asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(w), "v"(a), "i"(R),
+                         "i"(R + 15));
+    } else {
+        if constexpr (ZERO)
+            asm volatile("v_mfma_f32_32x32x16_f16 a[%c2:%c3], %0, %1, 0" ::"v"(w), "v"(a), "i"(R), "i"(R + 15));
+        else
+            asm volatile("v_mfma_f32_32x32x16_f16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(w), "v"(a), "i"(R),
+                         "i"(R + 15));
+    }
+}
+#endif
+
 // an empty asm on a wave-uniform value: the compiler can no longer see through it (no
 // hoisting or precomputing of what derives from it)
 __device__ __forceinline__ void launder_s(int& x) { asm volatile("" : "+s"(x)); }
@@ -348,6 +369,30 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         // builds): bit 0 no loop DMA, bit 1 no loop fragment reads
         constexpr bool DO_RD = RD && !(ABL & 2);
         constexpr bool DO_DMA = DMA && !(ABL & 1);
+#ifdef VP3D_ABLATION
+        if constexpr ((ABL & 64) != 0) {
+            // 32 x 32 blocks: 16 blocks x 2 k-steps of 16, one memory instruction ahead of each
+            // MFMA (the 16 reads on the even ones, the 16 DMA pieces on the odd ones)
+            static_for<32>([&](auto n_c) __attribute__((always_inline)) {
+                constexpr int n = decltype(n_c)::value;
+                constexpr int b = n >> 1, ks = n & 1, h = n >> 1;
+                if constexpr (DO_RD && (n & 1) == 0) {
+                    if constexpr (h < 8)
+                        fa[NXT][h] = *(const u32x4*)(rbuf + a_base + h * 2048 + fo);
+                    else
+                        fw[NXT][h - 8] = *(const u32x4*)(rbuf + w_base + (h - 8) * 2048 + fo);
+                }
+                if constexpr (DO_DMA && (n & 1) == 1) dma_piece(dbuf, std::integral_constant<int, h>{}, s, aoff, bs);
+                if constexpr (!DMA && (n & 1) == 1) {
+                    if (resp >= 0) res_piece(dbuf, std::integral_constant<int, h>{}, resp);
+                }
+                amma32<CT, 16 * b, ZERO>(fw[CUR][(b & 3) * 2 + ks], fa[CUR][(b >> 2) * 2 + ks]);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            if constexpr (RD) __builtin_amdgcn_s_waitcnt(kLgkm0);
+            return;
+        }
+#endif
         static_for<8>([&](auto i_c) __attribute__((always_inline)) {
             constexpr int I = decltype(i_c)::value;
             static_for<8>([&](auto j_c) __attribute__((always_inline)) {
@@ -1285,6 +1330,9 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p_in, Act compute, hipStrea
             case 1: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 1>), g, dim3(256), 0, stream, p); break;
             case 2: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 2>), g, dim3(256), 0, stream, p); break;
             case 3: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 3>), g, dim3(256), 0, stream, p); break;
+            case 64: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 64>), g, dim3(256), 0, stream, p); break;
+            case 65: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 65>), g, dim3(256), 0, stream, p); break;
+            case 66: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 66>), g, dim3(256), 0, stream, p); break;
             default: hipLaunchKernelGGL((conv_gemm_a4<__bf16, 4>), g, dim3(256), 0, stream, p); break;
         }
         return hipGetLastError();
