@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     u32x4 af[RB][NKS];
     u32x4 afl[X3 ? RB : 1][NKS];  // X3: the lo fragments
     constexpr float kBias = X3 ? 0.f : 1.f;  // the folded-shift column (16-bit path only)
-    bool x_ok = true;  // X3: every input value within the f16 range (NaN: false)
+    uint32_t x_hmax = 0;  // X3: max |hi| bits of the input rows (gemm::x3_hi_bad: inf / NaN)
     auto put = [&](int rb, int ks, const float (&v)[8]) {
         if constexpr (X3) {
             f16x8 h, l;
@@ -157,8 +157,10 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
             for (int e = 0; e < 8; ++e) {
                 h[e] = (f16)v[e];
                 l[e] = (f16)(v[e] - (float)h[e]);
-                x_ok = x_ok && __builtin_fabsf(v[e]) <= 65504.f;
             }
+            const u32x4 hw = __builtin_bit_cast(u32x4, h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x_hmax = gemm::x3_himax2(x_hmax, hw[e]);
             af[rb][ks] = __builtin_bit_cast(u32x4, h);
             afl[rb][ks] = __builtin_bit_cast(u32x4, l);
         } else {
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
     }
     exp_vm<0>();  // weight chunks 0 and 1 (and the A loads) landed
     __builtin_amdgcn_s_barrier();
-    if constexpr (X3) gemm::x3_range_flag(x_ok ? 0.f : __builtin_inff(), p.scale, p.N);
+    if constexpr (X3) gemm::x3_range_flag(gemm::x3_hi_bad(x_hmax) ? __builtin_inff() : 0.f, p.scale, p.N);
 
 #ifdef VP3D_ABLATION
     // measurement builds only (tools/ubench/expand_check): 2 = no global stores,

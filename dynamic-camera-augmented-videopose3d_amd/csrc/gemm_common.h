@@ -494,8 +494,19 @@ __device__ __forceinline__ uint32_t x3_hi2(float x0, float x1) {
 // the handle's fault word, whose device address the host keeps just past the layer's
 // scale_x3 vector (Layer::scale_x3[N .. N + 1], vp3d_capi.cpp upload_weights).
 __device__ __forceinline__ float x3_absmax2(float m, float a, float b) {
-    return __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(a), __builtin_fabsf(b)));
+    // (as asm: the compiler's fmaxf form canonicalises each operand first, 3 instructions)
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
 }
+// the input rows' check, on the packed hi halves: |hi| >= 0x7C00 is inf or NaN (what the
+// split of a value past the range, or of a NaN, leaves); one v_pk_max_u16 per pair
+__device__ __forceinline__ uint32_t x3_himax2(uint32_t m, uint32_t h) {
+    typedef unsigned short u16x2_ __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_, m),
+                                                                  __builtin_bit_cast(u16x2_, h & 0x7FFF7FFFu)));
+}
+__device__ __forceinline__ bool x3_hi_bad(uint32_t m) { return (m & 0xFFFFu) >= 0x7C00u || (m >> 16) >= 0x7C00u; }
 __device__ __forceinline__ void x3_range_flag(float m, const float* scale_x3, int n) {
     if (__builtin_expect(!(m <= 65504.f), 0)) {  // (a NaN input compares false too)
         unsigned* const f = *(unsigned* const*)(scale_x3 + n);

@@ -326,7 +326,7 @@ __global__ void pack_rows_x3_kernel(const float* __restrict__ x, const float* __
                                     int lead, int M, int T_out, int T_in, int stride, int cin, int K, int Kp,
                                     _Float16* __restrict__ out, unsigned* fault) {
     const int chunks = Kp >> 3;
-    bool ok = true;  // every value within the f16 range (NaN: false), else kFaultNonFinite
+    bool ok = true;  // every hi half finite (a value past the f16 range or a NaN: not), else kFaultNonFinite
     const int64_t total = (int64_t)M * chunks;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -363,7 +363,7 @@ __global__ void pack_rows_x3_kernel(const float* __restrict__ x, const float* __
         for (int e = 0; e < 8; ++e) {
             hi[e] = (_Float16)v[e];
             lo[e] = (_Float16)(v[e] - (float)hi[e]);
-            ok = ok && __builtin_fabsf(v[e]) <= 65504.f;
+            ok = ok && !((__builtin_bit_cast(unsigned short, hi[e]) & 0x7FFFu) >= 0x7C00u);  // inf / NaN hi
         }
         _Float16* o = out + (int64_t)m * 2 * Kp + (c >> 5) * 64 + (c & 31);
         *(h8*)o = hi;
