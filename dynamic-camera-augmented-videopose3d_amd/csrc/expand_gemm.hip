@@ -641,11 +641,14 @@ hipError_t launch_expand_gemm_x3(const ConvGemmParams& p, const GatherSrc* g, hi
     const int nks = (p.K + 31) / 32;
     const bool nt = (int64_t)p.M * p.ldy * 2 > (int64_t)256 << 20;
     const GatherSrc none{};
-    // RB 2 row blocks per wave, 2-chunk weight ring: 2 x 32 KB + 8 KB scale / shift (NKS 4),
-    // two workgroups per CU
+    // RB 3 row blocks per wave (each weight chunk staged into LDS serves 192 rows instead of
+    // 128), 2-chunk weight ring: 2 x 32 KB + 8 KB scale / shift (NKS 4), two workgroups per
+    // CU (206 / 250 VGPRs at NKS 4 / 5; RB 4 spills).  Same box vs RB 2: config-3 expand (the
+    // camera concat, NKS 5) 6.43-6.46 vs 6.75 ms, config 4 within noise; forwards
+    // bit-identical (profiles/r05_x3_expand_rb3_ab.txt)
     if (g)
-        return nt ? launch_rb_nt<f16, 2, true, true, 2, true>(p, *g, nks, stream)
-                  : launch_rb_nt<f16, 2, true, false, 2, true>(p, *g, nks, stream);
+        return nt ? launch_rb_nt<f16, 3, true, true, 2, true>(p, *g, nks, stream)
+                  : launch_rb_nt<f16, 3, true, false, 2, true>(p, *g, nks, stream);
     return nt ? launch_rb_nt<f16, 2, false, true, 2, true>(p, none, nks, stream)
               : launch_rb_nt<f16, 2, false, false, 2, true>(p, none, nks, stream);
 }
