@@ -20,7 +20,36 @@ HEADLINE = ["r02h_bench_bf16.json", "r02l_bench_default.json"]
 
 def _line(name):
     with open(os.path.join(PROFILES, name)) as f:
-        return json.loads(f.read().strip().splitlines()[-1])
+        text = f.read().strip()
+    try:
+        return json.loads(text)  # a pretty-printed line (profiles/r05final_*)
+    except json.JSONDecodeError:
+        return json.loads(text.splitlines()[-1])
+
+
+def test_current_default_line():
+    """The round's last default line (config 4, f16x3): the accurate path is `value`, priced at
+    the f16 peak / 3, with its legs -- bf16 / fp32, config 3, config 5 in fp32 and fp16, the
+    sequence mode -- and the north-star gate met by every accurate leg."""
+    d = _line("r05final_bench_default.json")
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert d["metric"] == base["metric"] and d["dtype"] == "f16x3" and d["n_gpus"] == 1
+    assert d["value"] == pytest.approx(65536 / (d["ms_per_step"] * 1e-3), rel=1e-3)
+    r = d["roofline"]
+    assert r["peak"] == pytest.approx(2500.0 / 3) and r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    assert r["achieved"] == pytest.approx(r["flop_per_launch"] / (r["avg_launch_ms"] * 1e-3) / 1e12, rel=1e-3)
+    p = d["parity"]
+    assert p["f16x3_meets_north_star_1e-4mm"] and p["f16x3_mpjpe_delta_mm"] <= 1e-4
+    assert p["fp32_mpjpe_delta_mm"] <= 1e-4 and p["reference_fp32_vs_fp64_mpjpe_delta_mm"] >= 0
+    assert d["config5"]["fp32"]["parity"]["meets_north_star_1e-4mm"]
+    for k in ("median", "p90", "p99"):
+        assert d["config5"]["fp32"]["serve_latency_us"][k] > 0
+    for k in ("f16x3", "fp32"):
+        assert d["sequence"][k]["meets_north_star_1e-4mm"] and d["sequence"][k]["roofline"]["frac"] > 0
+    assert d["config3"]["f16x3"]["mpjpe_delta_mm"] <= 1e-4
+    c = d["cpu_baseline"]
+    assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["affinity_cpus"] >= 1
 
 
 @pytest.mark.parametrize("name", HEADLINE)
