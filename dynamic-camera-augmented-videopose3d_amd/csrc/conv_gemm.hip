@@ -526,8 +526,10 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     const int gm = gemm_8p_mode();
     if ((gm == 5 || gm == 1) && conv_gemm_a4_eligible(p, a_type, out_type, compute) && conv_gemm_a4_fills(p))
         return launch_conv_gemm_a4(p, compute, stream);
-    if ((gm == 3 || (gm == 1 && p.dil == 1)) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
-        conv_gemm_q64_eligible(p, a_type, out_type, compute))
+    // q64 also below 384 tiles (round 5): it sums every output in a4's K order, so a layer gives
+    // the same bits at every batch size (the 128 x 128 kernel's order differs: config 4's block-4
+    // 1x1 at 8,192 windows per GPU broke bit identity across shard sizes)
+    if ((gm == 3 || (gm == 1 && p.dil == 1)) && conv_gemm_q64_eligible(p, a_type, out_type, compute))
         return launch_conv_gemm_q64(p, compute, stream);
     if (gemm_8p_env(p) && conv_gemm_big_eligible(p, a_type, out_type, compute) &&
         conv_gemm_8p_eligible(p, a_type, out_type, compute))

@@ -152,8 +152,16 @@ __device__ __forceinline__ float aread() {
 __device__ unsigned long long* g_a4_trace;
 #endif
 
-template <typename CT, int ABL, int X3 = 0, bool GD = true, bool SPLIT = false>
+// HN (half-N tiles, a launch's partial last round): 256 x 128 tiles -- each wave 128 rows x 64
+// channels, accumulator blocks (i, j < 4), 8 A + 4 W LDS-DMA pieces per K-tile -- over the
+// M-tiles from p.sk_full on, one unit per workgroup (no walk, no split, no residual).  Every
+// output keeps the whole tile's K order, so the same bits as a 256 x 256 tile.
+template <typename CT, int ABL, int X3 = 0, bool GD = true, bool SPLIT = false, bool HN = false>
 __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
+    static_assert(!HN || (GD && !SPLIT), "half-N tiles: grouped pieces, no split");
+    constexpr int TN = HN ? GN / 2 : GN;  // tile channels
+    constexpr int NJ = TN / 32;           // channel blocks of 16 per wave (two wave columns)
+    constexpr int WP = HN ? 4 : 8;        // W pieces per wave and K-tile
     // the accumulator file is this kernel's own from here on (see the header)
     asm volatile("" ::: A4_ALL_AGPRS);
     // a copy whose fields go through an empty asm every tile (below): values derived from them
@@ -175,9 +183,10 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         s_shift[i] = p.shift[i];
     }
 
-    const int ntn = p.N / GN;
+    const int ntn = p.N / TN;
     const int ntm = (p.M + GM - 1) / GM;
-    const int ntiles = ntm * ntn;
+    const int mt_base = HN ? p.sk_full : 0;  // HN: the first M-tile of the launch
+    const int ntiles = (ntm - mt_base) * ntn;
     const int nk_all = p.Kp / GK;  // >= 1
     // Work units: tile u < sk_full whole; with a split plan (ConvGemmParams::sk_*) the sk_left
     // tiles after them as S units each -- unit full + v: tile full + v % L, K range q = S - 1 -
@@ -246,8 +255,8 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         const int wg = xcd_remap(tix, ntiles);
         const int tile_m = wg / ntn;
         const int tile_n = wg - tile_m * ntn;
-        m0 = tile_m * GM;
-        n0 = tile_n * GN;
+        m0 = (mt_base + tile_m) * GM;
+        n0 = tile_n * TN;
         const int srow0 = src_row(p, m0);  // m0 < M; wave-uniform
         a_rsrc = make_rsrc((const char*)((const CT*)p.A + (int64_t)srow0 * p.lda) - kReb, 0x7FFFFFFFu);
         w_rsrc = make_rsrc((const char*)((const CT*)p.W + (int64_t)n0 * p.Kp) - kReb, 0x7FFFFFFFu);
@@ -263,12 +272,13 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int q = GD ? 8 * swv + i : swv + 4 * i;  // the piece's slot: rows 8q .. 8q + 7
+            const int qw = HN ? 4 * swv + (i & 3) : q;      // HN: 4 W slots per wave
             const int lci = GD ? (sln & 7) ^ (((i & 1) * 4 + (spr >> 1)) & 7) : lc;
             const int reb = GD ? kReb - (i & 3) * 1024 : 0;
             int m = m0 + 8 * q + spr;
             m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
             va[i] = (uint32_t)(((src_row(p, m) - srow0) * p.lda + lci * 8) * (int)sizeof(CT) + reb);
-            vw[i] = (uint32_t)(((8 * q + prow) * p.Kp + lci * 8) * (int)sizeof(CT) + reb);  // W rows padded
+            vw[i] = (uint32_t)(((8 * qw + prow) * p.Kp + lci * 8) * (int)sizeof(CT) + reb);  // W rows padded
             vr[i] = lres ? (uint32_t)(((res_row(p, m) - rrow0) * p.ldr + lci * 8) * (int)sizeof(CT) + reb) : 0u;
         }
     };
@@ -291,6 +301,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         int w = widu;
         launder_s(w);
         char* b = buf + 8 * w * 1024;
+        if constexpr (HN) return Bases{{b, b + 4096, buf + GW_OFF + 4 * w * 1024, nullptr}};
         return Bases{{b, b + 4096, b + GW_OFF, b + GW_OFF + 4096}};
     };
     auto piece_lds = [&](char* buf, int i) __attribute__((always_inline)) -> char* {
@@ -332,11 +343,11 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     auto stage_01 = [&]() __attribute__((always_inline)) {
         const int64_t o0 = a_koff(0);
         const Bases b0 = bases_of(buf0);
-        static_for<16>([&](auto i_c) __attribute__((always_inline)) { dma_piece(buf0, i_c, 0, o0, b0); });
+        static_for<8 + WP>([&](auto i_c) __attribute__((always_inline)) { dma_piece(buf0, i_c, 0, o0, b0); });
         if (nk > 1) {
             const int64_t o1 = a_koff(1);
             const Bases b1 = bases_of(buf1);
-            static_for<16>([&](auto i_c) __attribute__((always_inline)) { dma_piece(buf1, i_c, 1, o1, b1); });
+            static_for<8 + WP>([&](auto i_c) __attribute__((always_inline)) { dma_piece(buf1, i_c, 1, o1, b1); });
         }
     };
 
@@ -346,7 +357,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     int fo0 = (lane & 15) * 128 + (((lane >> 4) ^ fsw) << 4);
     int fo1 = (lane & 15) * 128 + ((((lane >> 4) + 4) ^ fsw) << 4);
     int a_base = wr * 128 * 128;
-    int w_base = GW_OFF + wc * 128 * 128;
+    int w_base = GW_OFF + wc * (TN / 2) * 128;
 
     u32x4 fa[2][8], fw[2][8];  // [set][block]
 
@@ -370,7 +381,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         constexpr bool DO_RD = RD && !(ABL & 2);
         constexpr bool DO_DMA = DMA && !(ABL & 1);
 #ifdef VP3D_ABLATION
-        if constexpr ((ABL & 64) != 0) {
+        if constexpr ((ABL & 64) != 0 && !HN) {
             // 32 x 32 blocks: 16 blocks x 2 k-steps of 16, one memory instruction ahead of each
             // MFMA (the 16 reads on the even ones, the 16 DMA pieces on the odd ones)
             static_for<32>([&](auto n_c) __attribute__((always_inline)) {
@@ -395,14 +406,24 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
 #endif
         static_for<8>([&](auto i_c) __attribute__((always_inline)) {
             constexpr int I = decltype(i_c)::value;
-            static_for<8>([&](auto j_c) __attribute__((always_inline)) {
+            static_for<NJ>([&](auto j_c) __attribute__((always_inline)) {
                 constexpr int J = decltype(j_c)::value;
-                if constexpr (DO_RD && J == 0) fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
-                if constexpr (DO_RD && J == 4) fw[NXT][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo);
-                if constexpr (DO_DMA && (J == 2 || J == 6))
-                    dma_piece(dbuf, std::integral_constant<int, 2 * I + J / 4>{}, s, aoff, bs);
-                if constexpr (!DMA && (J == 2 || J == 6)) {
-                    if (resp >= 0) res_piece(dbuf, std::integral_constant<int, 2 * I + J / 4>{}, resp);
+                if constexpr (HN) {
+                    // 4 MFMAs per row block: A read, DMA piece I (A), W read (I < 4), piece 8 + I (W)
+                    if constexpr (DO_RD && J == 0) fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
+                    if constexpr (DO_DMA && J == 1) dma_piece(dbuf, std::integral_constant<int, I>{}, s, aoff, bs);
+                    if constexpr (DO_RD && J == 2 && I < 4)
+                        fw[NXT][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo);
+                    if constexpr (DO_DMA && J == 3 && I < 4)
+                        dma_piece(dbuf, std::integral_constant<int, 8 + I>{}, s, aoff, bs);
+                } else {
+                    if constexpr (DO_RD && J == 0) fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
+                    if constexpr (DO_RD && J == 4) fw[NXT][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo);
+                    if constexpr (DO_DMA && (J == 2 || J == 6))
+                        dma_piece(dbuf, std::integral_constant<int, 2 * I + J / 4>{}, s, aoff, bs);
+                    if constexpr (!DMA && (J == 2 || J == 6)) {
+                        if (resp >= 0) res_piece(dbuf, std::integral_constant<int, 2 * I + J / 4>{}, resp);
+                    }
                 }
                 amma<CT, 4 * (8 * I + J), ZERO>(fw[CUR][J], fa[CUR][I]);
                 __builtin_amdgcn_sched_barrier(0);
@@ -526,7 +547,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
     };
     auto epi_fast = [&](auto h_c, bool with_res, int em0, int en0, __amdgpu_buffer_rsrc_t y_rsrc, int own_si) __attribute__((always_inline)) {
         constexpr int H = decltype(h_c)::value;
-        const int nw = en0 + wc * 128 + 64 * H;
+        const int nw = en0 + wc * (TN / 2) + 64 * H;
         f32x2 sc[4][2], sh[4][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -599,13 +620,18 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         // across it (past 256 VGPRs, into the accumulator file)
         launder_lane_consts(prow, lc, fsw, fo0, fo1, a_base, w_base, grp, c0);
         launder_params(p);
-        const int next = tix + (int)gridDim.x;
+        const int next = HN ? nunits : tix + (int)gridDim.x;  // (HN: one unit per workgroup)
         const bool has_next = next < nunits;
         res0 = lres ? 0 : -1;
         res1 = lres ? 1 : -1;
         if (first) {
             if (nk > 1)
-                asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // K-tile 0 landed (younger: K-tile 1)
+            {
+                if constexpr (HN)
+                    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // K-tile 0 landed (younger: K-tile 1)
+                else
+                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            }
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // scale / shift stores
@@ -630,7 +656,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             fa[0][i] = *(const u32x4*)(buf0 + a_base + i * 2048 + fo0);
-            fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
+            if (!HN || i < 4) fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
         }
         if constexpr (X3 != 0) {
             // ---- split fp16 (VP3D_DTYPE_F16X3): rows hold every f32 value as f16 halves, each
@@ -654,7 +680,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             // 128-byte group s of each row, 16-byte chunks with the A pieces' swizzle.  Per-lane
             // source offsets vr[i] (the A pieces' rows, computed once the A / W DMA offsets are
             // dead: the K loop has no VGPRs to spare) ----
-            const bool xres = X3 == 1 && !SPLIT && !(ABL & 40) && p.R != nullptr && role != kHelper && nk >= 3;
+            const bool xres = X3 == 1 && !SPLIT && !HN && !(ABL & 40) && p.R != nullptr && role != kHelper && nk >= 3;
             __amdgpu_buffer_rsrc_t xr_rsrc;
             auto xres_prep = [&]() __attribute__((always_inline)) {
                 // lane values through an empty asm: nothing derived from them is hoisted out of
@@ -692,30 +718,34 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 constexpr bool DO_DMA = decltype(dma_c)::value && !(ABL & 1);
                 const int64_t aoff = DO_DMA ? a_koff(s) : 0;
                 const Bases bs = DO_DMA ? bases_of(dbuf) : Bases{};
+                // (HN: 4 channel blocks; the W reads / pieces move from J = 4 / 2 to 2 / 3, I < 4)
+                constexpr int JW = HN ? 2 : 4;
                 static_for<8>([&](auto i_c) __attribute__((always_inline)) {
                     constexpr int I = decltype(i_c)::value;
-                    static_for<8>([&](auto j_c) __attribute__((always_inline)) {
+                    constexpr bool WI = !HN || I < 4;  // a W block to read / a W piece to issue
+                    static_for<NJ>([&](auto j_c) __attribute__((always_inline)) {
                         constexpr int J = decltype(j_c)::value;
                         if constexpr (KIND == 0) {
                             if constexpr (DO_RD && J == 0)
                                 fa[1 - H][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo1);
-                            if constexpr (DO_RD && J == 4)
+                            if constexpr (DO_RD && J == JW && WI)
                                 fw[1][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo1);
                             amma<CT, 4 * (8 * I + J), ZERO>(fw[0][J], fa[H][I]);
                         } else if constexpr (KIND == 1) {
                             if constexpr (DO_RD && J == 0 && I > 0)
                                 fa[1 - H][I - 1] = *(const u32x4*)(rbuf + a_base + (I - 1) * 2048 + fo0);
-                            if constexpr (DO_DMA && J == 4) dma_piece(dbuf, i_c, s, aoff, bs);
-                            if constexpr (RQ >= 0 && (J == 2 || J == 6))
+                            if constexpr (DO_DMA && J == JW) dma_piece(dbuf, i_c, s, aoff, bs);
+                            if constexpr (RQ >= 0 && !HN && (J == 2 || J == 6))
                                 xres_piece(rqbuf, i_c, std::integral_constant<int, J / 4>{}, RQ, 0);
                             amma<CT, 4 * (8 * I + J), false>(fw[0][J], fa[1 - H][I]);
                         } else {
                             if constexpr (DO_RD && J == 0 && I == 0)
                                 fa[1 - H][7] = *(const u32x4*)(rbuf + a_base + 7 * 2048 + fo0);
-                            if constexpr (DO_RD && J == 4) fw[0][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo0);
-                            if constexpr (DO_DMA && J == 2)
+                            if constexpr (DO_RD && J == JW && WI)
+                                fw[0][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo0);
+                            if constexpr (DO_DMA && J == (HN ? 3 : 2) && WI)
                                 dma_piece(dbuf, std::integral_constant<int, 8 + I>{}, s, aoff, bs);
-                            if constexpr (RQ >= 0 && (J == 2 || J == 6))
+                            if constexpr (RQ >= 0 && !HN && (J == 2 || J == 6))
                                 xres_piece(rqbuf, i_c, std::integral_constant<int, J / 4>{}, RQ, 0);
                             amma<CT, 4 * (8 * I + J), false>(fw[1][J], fa[H][I]);
                         }
@@ -836,7 +866,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                                __attribute__((always_inline)) {
                 constexpr int HH = decltype(hh_c)::value;
                 constexpr bool WITH_R = decltype(wr_c)::value && !(ABL & 8);
-                const int nw = en0 + ewc * 128 + 64 * HH;
+                const int nw = en0 + ewc * (TN / 2) + 64 * HH;
                 f32x2 sc[4][2], sh[4][2];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -989,7 +1019,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 // front -- epilogue_tp_x3 loads it one row block ahead, a latency per row block
                 auto global_half = [&](auto hh_c) __attribute__((always_inline)) {
                     constexpr int HH = decltype(hh_c)::value;
-                    const int nw = en0 + ewc * 128 + 64 * HH;
+                    const int nw = en0 + ewc * (TN / 2) + 64 * HH;
                     u32x4 rr[8][2][2];
                     if (has_r && !(ABL & 8)) {
 #pragma unroll
@@ -1012,7 +1042,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 };
                 if constexpr ((ABL & 32) == 0) {  // (measurement builds: ABL bit 5 skips the epilogue)
                     global_half(std::integral_constant<int, 0>{});
-                    global_half(std::integral_constant<int, 1>{});
+                    if constexpr (!HN) global_half(std::integral_constant<int, 1>{});
                 }
                 if (erole == kOwner) owner_done(esidx);
             }
@@ -1094,7 +1124,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         const size_t y_rest = (size_t)(p.M - em0) * p.ldy * sizeof(CT);
         const __amdgpu_buffer_rsrc_t y_rsrc =
             make_rsrc((const CT*)p.Y + (size_t)em0 * p.ldy, clamp_range31(y_rest));
-        if (elres) {
+        if (!HN && elres) {
             // residual part h into registers once landed (every wave's pieces: after the
             // barrier), then its buffer takes the next tile's K-tile h (nk even: part h sits in
             // buffer h) before the half-h stores: issue order part 0, part 1, K-tile 0, H0
@@ -1127,7 +1157,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             part(H1{});
         } else {  // no residual (the eligibility check leaves no residual with nk < 3)
             epi_fast(H0{}, false, em0, en0, y_rsrc, own_si);
-            epi_fast(H1{}, false, em0, en0, y_rsrc, own_si);
+            if constexpr (!HN) epi_fast(H1{}, false, em0, en0, y_rsrc, own_si);
         }
         if (erole == kOwner) owner_done(esidx);
         prev_lres = elres;
@@ -1224,8 +1254,34 @@ static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk, bool need_ws = 
 
 // the tile count from which a4 is the kernel of a 16-bit layer (fewer: q64 / the 128 x 128
 // kernel), unless a split plan fills the chip (config 4's block 4 at N = 8: 128 tiles)
+// Half-N plan of a launch's partial last round (round 5): with L <= CUs / 2 tiles past the last
+// whole round, their L / 4 M-tiles (N = 1024) run as 2L units of 256 x 128 in a second launch
+// (conv_gemm_a4<..., HN>) after the whole rounds -- every output in the whole tile's K order,
+// so bit-identical across batch sizes (split-K sums a tile's K in S chains).  Layers without a
+// residual (the k3 convs, whose tile walk is off): the 1x1 + residual layers keep whole tiles.
+// Measured same box (profiles/r05_a4_half_n_tail_ab.txt): f16x3 at 8,192 windows every k3
+// faster than split-K (block 4 0.122 vs 0.153 ms, block 3 0.347 vs 0.365), step +0.6..1.8 %;
+// 16-bit operands only where the layer has no whole round (block 4 at 8,192: 0.060 vs 0.085
+// ms; 1,024 windows +8 %) -- after whole rounds their half tiles, DMA-issue-bound at 12 pieces
+// per 64 MFMAs, ran no faster than the whole-tile round (block 3 at 8,192: 0.157 vs 0.148).
+// VP3D_A4_HN=0 (measurement) turns it off; VP3D_A4_SPLIT=2 (the split-K test) takes
+// precedence.  Returns the M-tiles of the tail (0: none).
+static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3) {
+    const char* e = getenv("VP3D_A4_HN");
+    if (e && e[0] == '0') return 0;
+    const char* sp = getenv("VP3D_A4_SPLIT");
+    if (sp && atoi(sp) == 2) return 0;
+    const int ncu = a4_cus();
+    const int ntn = p.N / GN;
+    if (p.R != nullptr || ncu <= 0 || ntn <= 0) return 0;
+    const int L = ntiles % ncu;
+    if (L == 0 || 2 * L > ncu || L % ntn != 0 || (!x3 && ntiles >= ncu)) return 0;
+    return L / ntn;
+}
+
 bool conv_gemm_a4_would_split(const ConvGemmParams& p) {
     const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+    if (a4_hn_tail(p, ntiles, true) > 0) return false;  // (the split workspace: f16x3 layers)
     ConvGemmParams q = p;
     a4_split_plan(q, ntiles, p.Kp / GK, false);
     return q.sk_split > 1;
@@ -1234,6 +1290,7 @@ bool conv_gemm_a4_would_split(const ConvGemmParams& p) {
 bool conv_gemm_a4_fills(const ConvGemmParams& p) {
     const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
     if (ntiles >= 384) return true;
+    if (a4_hn_tail(p, ntiles, false) > 0) return true;  // the 16-bit dispatch: the layer as 2L half tiles
     ConvGemmParams q = p;
     a4_split_plan(q, ntiles, p.Kp / GK);
     return q.sk_split > 1;
@@ -1245,6 +1302,24 @@ static void a4_launch(const ConvGemmParams& p, dim3 grid, bool split, hipStream_
         hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, true>), grid, dim3(256), 0, stream, p);
     else
         hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), grid, dim3(256), 0, stream, p);
+}
+
+// the whole rounds (M-tiles below ntm - mt_tail, if any) then the tail as half-N units
+template <typename CT, int X3>
+static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t stream) {
+    const int ntm = (p.M + GM - 1) / GM;
+    const int mt0 = ntm - mt_tail;
+    if (mt0 > 0) {
+        ConvGemmParams q = p;
+        q.M = mt0 * GM;
+        q.sk_split = q.sk_full = q.sk_left = 0;
+        hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), dim3(mt0 * (p.N / GN)), dim3(256), 0, stream, q);
+    }
+    ConvGemmParams t = p;
+    t.sk_split = t.sk_left = 0;
+    t.sk_full = mt0;  // the HN launch's first M-tile
+    hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false, true>), dim3(mt_tail * (p.N / (GN / 2))), dim3(256), 0,
+                       stream, t);
 }
 
 #ifdef VP3D_ABLATION
@@ -1261,11 +1336,21 @@ hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p_in, bool out_f32, hipS
     // VP3D_A4_WALK 0: never, 2: every layer
     const int ntiles = ((p_in.M + GM - 1) / GM) * (p_in.N / GN);
     ConvGemmParams p = p_in;
+    const char* we = getenv("VP3D_A4_WALK");
+    const int walk_mode = we ? atoi(we) : 1;
+    const int hn_tail = walk_mode == 2 ? 0 : a4_hn_tail(p, ntiles, true);
+#ifndef VP3D_ABLATION
+    if (hn_tail > 0) {
+        if (out_f32)
+            a4_launch_hn<_Float16, 2>(p, hn_tail, stream);
+        else
+            a4_launch_hn<_Float16, 1>(p, hn_tail, stream);
+        return hipGetLastError();
+    }
+#endif
     a4_split_plan(p, ntiles, p.Kp / GK);
     const bool split = p.sk_split > 1;
     const int nunits = split ? p.sk_full + p.sk_split * p.sk_left : ntiles;
-    const char* we = getenv("VP3D_A4_WALK");
-    const int walk_mode = we ? atoi(we) : 1;
     const int ncu = a4_cus();
     const bool walk = walk_mode > 0 && (p.R != nullptr || walk_mode == 2) && ncu > 0 && nunits > ncu;
     const dim3 grid(walk ? ncu : nunits);
@@ -1310,6 +1395,16 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p_in, Act compute, hipStrea
     const int ncu = a4_cus();
     const int nk = p_in.Kp / GK;
     ConvGemmParams p = p_in;
+#ifndef VP3D_ABLATION
+    const int hn_tail = walk_mode == 2 ? 0 : a4_hn_tail(p, ntiles, false);
+    if (hn_tail > 0) {
+        if (compute == Act::BF16)
+            a4_launch_hn<__bf16, 0>(p, hn_tail, stream);
+        else
+            a4_launch_hn<_Float16, 0>(p, hn_tail, stream);
+        return hipGetLastError();
+    }
+#endif
     a4_split_plan(p, ntiles, nk);
     const bool split = p.sk_split > 1;
     const int nunits = split ? p.sk_full + p.sk_split * p.sk_left : ntiles;

@@ -161,6 +161,33 @@ def test_gemm_a4_bit_identical_to_q64(dtype, walk, monkeypatch):
     _check(ys["a4"][sel], ref, gt, dtype)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f16x3"])
+def test_a4_half_n_tail_bit_identical(dtype, monkeypatch):
+    """B = 8,192: every block conv leaves 128 tiles past its whole rounds (block 4: 128 tiles in
+    all); the k3 convs run them as 256 half-N tiles of 256 x 128 (conv_gemm_a4 HN, a second
+    launch) -- the same bits as q64's whole tiles and as a4's own whole tiles (VP3D_A4_HN=0,
+    no split-K)."""
+    model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
+    x = synth.normalized_windows(1, "x8192_243", 8192, 243)
+    model.cuda().set_compute_dtype(dtype)
+    xd = torch.from_numpy(x).cuda()
+    ys = {}
+    for name, env in (("hn", {}), ("whole", {"VP3D_A4_HN": "0", "VP3D_A4_SPLIT": "0"}), ("q64", {"VP3D_GEMM": "q64"})):
+        for k in ("VP3D_A4_HN", "VP3D_A4_SPLIT", "VP3D_GEMM"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with torch.no_grad():
+            ys[name] = model(xd).cpu().numpy()
+    assert np.isfinite(ys["hn"]).all()
+    assert np.array_equal(ys["hn"], ys["whole"]), np.abs(ys["hn"] - ys["whole"]).max()
+    assert np.array_equal(ys["hn"], ys["q64"]), np.abs(ys["hn"] - ys["q64"]).max()
+    sel = np.r_[0:32, 8160:8192]
+    ref = lifter_forward(sd, x[sel], [3, 3, 3, 3, 3], causal=False, strided=True, dense=False).numpy()
+    gt = synth.gt_poses(3, "gt", 64, 17).reshape(ref.shape)
+    _check(ys["hn"][sel], ref, gt, dtype)
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 def test_dilated_seq_a4_bit_identical_to_q64(dtype, monkeypatch):
     """VP3D_GEMM=a4 puts the dilated k3 convs of a long sequence (taps d rows apart: the tile's
@@ -293,7 +320,7 @@ def test_a4_split_k_last_round(dtype, monkeypatch):
     the whole-tile run (VP3D_A4_SPLIT=0): f16x3 within 1e-6 m (only the partial sums' rounding
     differs), bf16 within its coordinate gate; both against the oracle on the first and last
     64 windows under their dtype's gates."""
-    monkeypatch.setenv("VP3D_A4_SPLIT", "2")  # every layer it fits (default: the f16x3 k3 convs)
+    monkeypatch.setenv("VP3D_A4_SPLIT", "2")  # every layer it fits (default: none -- half-N tails)
     model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
     B = 8192
     x = synth.normalized_windows(5, "x8192_243", B, 243)
@@ -318,11 +345,13 @@ def test_a4_split_k_last_round(dtype, monkeypatch):
 def test_a4_split_k_timeout_raises(monkeypatch):
     """Fault injection for the split-K owner's bounded wait (conv_gemm_a4.hip owner_wait):
     VP3D_A4_SPLIT_DROP=1 makes every helper unit skip its count, so each owner tile of the
-    partial last round (f16x3 k3 convs at 8,192 windows) gives up after its bound
+    partial last round (VP3D_A4_SPLIT=2: every conv at 8,192 windows) gives up after its bound
     (VP3D_A4_SPLIT_SPIN_TICKS, 1 ms here).  The fault must surface, not pass as poses:
     the next forward on the handle is refused and sync_status raises RuntimeError; after
     sync_status cleared it (tile flags re-zeroed) the handle reproduces the good poses bit
     for bit."""
+    # split-K wherever it fits (the default runs these tails as half-N tiles, no split)
+    monkeypatch.setenv("VP3D_A4_SPLIT", "2")
     model, _ = make_model(True, (3, 3, 3, 3, 3), False, 1024)
     B = 8192
     x = torch.from_numpy(synth.normalized_windows(5, "x8192_243", B, 243)).cuda()
@@ -330,7 +359,7 @@ def test_a4_split_k_timeout_raises(monkeypatch):
     lifter = model.native_lifter()
     with torch.no_grad():
         good = model(x).cpu().numpy()
-        lifter.sync_status()  # no fault on the default path
+        lifter.sync_status()  # no fault on the split path
         monkeypatch.setenv("VP3D_A4_SPLIT_DROP", "1")
         monkeypatch.setenv("VP3D_A4_SPLIT_SPIN_TICKS", "100000")
         model(x)

@@ -85,3 +85,21 @@ def test_config4_two_ranks_bit_equal(tmp_path, dtype):
     want = float(np.mean(np.linalg.norm(y_full.astype(np.float64) - gt, axis=-1)))
     for p in parts:
         assert abs(float(p["g"]) - want) <= 1e-12 * max(1.0, want)
+
+
+@pytest.mark.parametrize("dtype", ["f16x3", "fp32"])
+def test_config4_eight_shards_bit_equal(dtype):
+    """Config 4 at N = 8 (8,192 windows per rank), the shards run one after another on the one
+    GPU: their concatenation is bit-equal to the unsharded 65,536-window forward.  At 8,192
+    windows every conv leaves a partial last round (128 tiles past the whole rounds), which
+    runs as 256 x 128 half-N tiles in the whole tile's K order (conv_gemm_a4 HN) -- not as
+    split-K chains, which gave up bit identity across shard sizes; layers under 384 tiles run
+    on q64 (a4's K order) and the exact f32 shrink is the same bits narrow or tiled.  (The
+    16-bit dtypes' shrink is not: its narrow kernel for < 32,768 rows sums K in another order
+    than the tile kernel)"""
+    dev = torch.device("cuda", 0)
+    y_full, _, _ = _run_shard(0, 1, dev, dtype)
+    parts = [_run_shard(r, 8, dev, dtype) for r in range(8)]
+    assert [(s, e) for _, s, e in parts] == [(r * G // 8, (r + 1) * G // 8) for r in range(8)]
+    y_cat = torch.cat([y for y, _, _ in parts]).cpu().numpy()
+    assert np.array_equal(y_cat, y_full.cpu().numpy())
