@@ -1198,6 +1198,8 @@ bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
     return (size_t)p.N * p.Kp < (1u << 31);
 }
 
+static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3);
+
 bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32) {
     if (p.Ktap % GK != 0 || p.Kp % GK != 0 || p.lda % 8 != 0) return false;
     if (p.N % GN != 0 || p.N > GMAXN || p.ldy % (out_f32 ? 4 : 8) != 0 || (p.R && p.ldr % 8 != 0)) return false;
@@ -1205,8 +1207,9 @@ bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32) {
         (reinterpret_cast<uintptr_t>(p.W) & 15) || (p.R && (reinterpret_cast<uintptr_t>(p.R) & 15)))
         return false;
     // enough tiles to fill the CUs (as the 16-bit dispatch: >= 384 tiles of 256 x 256), or a
-    // split plan that does
-    if (!conv_gemm_a4_fills(p)) return false;
+    // half-N or split plan that does
+    const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
+    if (!conv_gemm_a4_fills(p) && a4_hn_tail(p, ntiles, true) == 0) return false;
     return (size_t)p.N * p.Kp < (1u << 31);
 }
 
@@ -1258,9 +1261,10 @@ static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk, bool need_ws = 
 // whole round, their L / 4 M-tiles (N = 1024) run as 2L units of 256 x 128 in a second launch
 // (conv_gemm_a4<..., HN>) after the whole rounds -- every output in the whole tile's K order,
 // so bit-identical across batch sizes (split-K sums a tile's K in S chains).  Layers without a
-// residual (the k3 convs, whose tile walk is off): the 1x1 + residual layers keep whole tiles.
-// Measured same box (profiles/r05_a4_half_n_tail_ab.txt): f16x3 at 8,192 windows every k3
-// faster than split-K (block 4 0.122 vs 0.153 ms, block 3 0.347 vs 0.365), step +0.6..1.8 %;
+// residual, and the f16x3 1x1 + residual layers (half tiles load their residual half globally;
+// the whole rounds before them are walked as usual).  Measured same box
+// (profiles/r05_a4_half_n_tail_ab.txt): f16x3 at 8,192 windows every conv faster than split-K /
+// whole tiles (block-4 k3 0.122 vs 0.151 ms, 1x1 0.056 vs 0.079), step +2.4 % (0.946 of 65,536);
 // 16-bit operands only where the layer has no whole round (block 4 at 8,192: 0.060 vs 0.085
 // ms; 1,024 windows +8 %) -- after whole rounds their half tiles, DMA-issue-bound at 12 pieces
 // per 64 MFMAs, ran no faster than the whole-tile round (block 3 at 8,192: 0.157 vs 0.148).
@@ -1273,7 +1277,8 @@ static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3) {
     if (sp && atoi(sp) == 2) return 0;
     const int ncu = a4_cus();
     const int ntn = p.N / GN;
-    if (p.R != nullptr || ncu <= 0 || ntn <= 0) return 0;
+    // (the f16x3 1x1 + residual layers too: their half tiles load the residual half globally)
+    if ((p.R != nullptr && !x3) || ncu <= 0 || ntn <= 0) return 0;
     const int L = ntiles % ncu;
     if (L == 0 || 2 * L > ncu || L % ntn != 0 || (!x3 && ntiles >= ncu)) return 0;
     return L / ntn;
@@ -1304,16 +1309,19 @@ static void a4_launch(const ConvGemmParams& p, dim3 grid, bool split, hipStream_
         hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), grid, dim3(256), 0, stream, p);
 }
 
-// the whole rounds (M-tiles below ntm - mt_tail, if any) then the tail as half-N units
+// the whole rounds (M-tiles below ntm - mt_tail, if any; walked by one workgroup per CU when
+// `walk_cus` > 0) then the tail as half-N units
 template <typename CT, int X3>
-static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t stream) {
+static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t stream, int walk_cus = 0) {
     const int ntm = (p.M + GM - 1) / GM;
     const int mt0 = ntm - mt_tail;
     if (mt0 > 0) {
         ConvGemmParams q = p;
         q.M = mt0 * GM;
         q.sk_split = q.sk_full = q.sk_left = 0;
-        hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), dim3(mt0 * (p.N / GN)), dim3(256), 0, stream, q);
+        const int tiles = mt0 * (p.N / GN);
+        const dim3 g(walk_cus > 0 && tiles > walk_cus ? walk_cus : tiles);
+        hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), g, dim3(256), 0, stream, q);
     }
     ConvGemmParams t = p;
     t.sk_split = t.sk_left = 0;
@@ -1341,10 +1349,12 @@ hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p_in, bool out_f32, hipS
     const int hn_tail = walk_mode == 2 ? 0 : a4_hn_tail(p, ntiles, true);
 #ifndef VP3D_ABLATION
     if (hn_tail > 0) {
+        // the whole rounds walked as without the tail (the 1x1 + residual layers)
+        const int wc = walk_mode > 0 && p.R != nullptr ? a4_cus() : 0;
         if (out_f32)
-            a4_launch_hn<_Float16, 2>(p, hn_tail, stream);
+            a4_launch_hn<_Float16, 2>(p, hn_tail, stream, wc);
         else
-            a4_launch_hn<_Float16, 1>(p, hn_tail, stream);
+            a4_launch_hn<_Float16, 1>(p, hn_tail, stream, wc);
         return hipGetLastError();
     }
 #endif
