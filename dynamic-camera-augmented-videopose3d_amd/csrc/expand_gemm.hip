@@ -383,22 +383,9 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                         ol[e] = gemm::x3_split_lo2(oh[e], v[2 * e], v[2 * e + 1]);
                         vmax = gemm::x3_absmax2(vmax, v[2 * e], v[2 * e + 1]);
                     }
-                    if constexpr (NKS > 4) {
-                        // (the camera-concat shape: the two 64-byte halves of 16 lines per
-                        // instruction measured faster there, 7.54 vs 7.74 ms)
-                        const int m = m_wave + rb * 16 + r16;
-                        if (m < p.M) {
-                            u32x4* dst = (u32x4*)((f16*)p.Y + (int64_t)m * p.ldy + 2 * n0 + 64 * jp + c0);
-                            if constexpr (NT) {
-                                __builtin_nontemporal_store(oh, dst);
-                                __builtin_nontemporal_store(ol, dst + 4);
-                            } else {
-                                dst[0] = oh;
-                                dst[4] = ol;
-                            }
-                        }
-                        continue;
-                    }
+                    // (the camera-concat shape too since round 5: it had kept half lines of 16 rows
+                    // per instruction, nontemporal; whole lines at 3 row blocks per wave: config-3
+                    // expand 6.24-6.25 vs 6.37-6.40 ms, profiles/r05_x3_expand_rb_policy_ab.txt)
                     // whole 128-byte lines per store instruction: the line of row r holds its 32
                     // hi then 32 lo channels; lanes of rows 8-15 of the 16 trade with rows 0-7 (DPP
                     // row_ror:8, written only into the bank half that takes the partner's value)
@@ -646,9 +633,26 @@ hipError_t launch_expand_gemm_x3(const ConvGemmParams& p, const GatherSrc* g, hi
     // CU (206 / 250 VGPRs at NKS 4 / 5; RB 4 spills).  Same box vs RB 2: config-3 expand (the
     // camera concat, NKS 5) 6.43-6.46 vs 6.75 ms, config 4 within noise; forwards
     // bit-identical (profiles/r05_x3_expand_rb3_ab.txt)
-    if (g)
-        return nt ? launch_rb_nt<f16, 3, true, true, 2, true>(p, *g, nks, stream)
-                  : launch_rb_nt<f16, 3, true, false, 2, true>(p, *g, nks, stream);
+    // RB 3 or 2 by the rounds each leaves (a partial last round of few row blocks is split
+    // into channel-range workgroups, launch_rb_nt): per-round cost ~ RB, the last round costs
+    // 1 / S of a round -- 8,192 windows: RB 2 (10 rounds + 1/8) over RB 3 (6 + a 0.75 round)
+    const int slots = exp_slots();
+    auto cost = [&](int rb) {
+        const int nrb = (p.M + 64 * rb - 1) / (64 * rb);
+        if (slots <= 0) return (double)nrb * rb;
+        const int full = nrb / slots, left = nrb % slots;
+        int S = left > 0 ? slots / left : 1;
+        S = S > 8 ? 8 : S;
+        return (full + (left > 0 ? 1.0 / S : 0.0)) * rb;
+    };
+    const bool rb3 = cost(3) <= cost(2) + 1e-9;
+    if (g) {
+        if (rb3)
+            return nt ? launch_rb_nt<f16, 3, true, true, 2, true>(p, *g, nks, stream)
+                      : launch_rb_nt<f16, 3, true, false, 2, true>(p, *g, nks, stream);
+        return nt ? launch_rb_nt<f16, 2, true, true, 2, true>(p, *g, nks, stream)
+                  : launch_rb_nt<f16, 2, true, false, 2, true>(p, *g, nks, stream);
+    }
     return nt ? launch_rb_nt<f16, 2, false, true, 2, true>(p, none, nks, stream)
               : launch_rb_nt<f16, 2, false, false, 2, true>(p, none, nks, stream);
 }
