@@ -411,42 +411,38 @@ __global__ __launch_bounds__(256) void conv_gemm_narrow(ConvGemmParams p) {
 }
 
 // Exact-f32 narrow layers (N <= 64: the shrink conv of the fp32 and split-fp16 paths,
-// TemporalModel.py:33 / :74; the sequence lifters' 51-wide output Linear): one wave per 16 rows
-// x 64 columns, operands straight from global memory (each lane: a 16-byte run of its row's K
-// and of 4 weight rows -- the weight rows stay in L1/L2 for every wave), the MFMA k order of
+// TemporalModel.py:33 / :74; the sequence lifters' 51-wide output Linear): one workgroup per 16
+// rows, one wave per 16 of its <= 64 columns, operands straight from global memory (each lane: a
+// 16-byte run of its row's K and of its weight row -- the weight rows stay in L1/L2), the MFMA k order of
 // conv_gemm_f32 (v_mfma_f32_16x16x4_f32 s = 0..3 over the 16-deep step, lane group c holding
 // k = 16 kt + 4 c + s), so the same bits.  conv_gemm_f32 ran these on 128 x 128 tiles: 64 of
 // them at B = 8,192 windows, a 64-step K loop with a barrier per step on 64 CUs: 93 vs 54 us,
 // and 38 us with an 8-step operand ring (profiles/r04final_narrow_shrink_ring_ab.txt).  From 256
 // tiles of 128 rows on, the tile kernel keeps up (B = 65,536: 0.167 vs 0.163 ms narrow).
-__global__ __launch_bounds__(64) void conv_gemm_f32_narrow(ConvGemmParams p) {
-    const int lane = threadIdx.x;
+__global__ __launch_bounds__(256) void conv_gemm_f32_narrow(ConvGemmParams p) {
+    // (round 5) one wave per 16 rows x 16 columns: the 4 waves of a workgroup take the 4
+    // column blocks of the same 16 rows (A from L1 for three of them), 4x the waves in flight
+    // for the loads' latency; each output's MFMA chain unchanged, so the same bits
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (16 * wid >= p.N) return;  // (wave-uniform) no columns in this block
     const int c = lane >> 4, r = lane & 15;
     const int m0 = blockIdx.x * 16;
     const int m = m0 + r;
     const bool mv = m < p.M;
     const float* const arow = (const float*)p.A + (int64_t)(mv ? src_row(p, m) : 0) * p.lda + 4 * c;
-    const float* wrow[4];
-    bool nv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = 16 * j + r;
-        nv[j] = n < p.N;
-        wrow[j] = (const float*)p.W + (int64_t)(nv[j] ? n : 0) * p.Kp + 4 * c;
-    }
-    f32x4 acc[1][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int n = 16 * wid + r;
+    const bool nv = n < p.N;
+    const float* const wrow = (const float*)p.W + (int64_t)(nv ? n : 0) * p.Kp + 4 * c;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nk = p.K / 16;
-    // a ring of kDepth K-steps of operands in flight: one step's 16 MFMAs (~130 cycles) are far
-    // shorter than a global load, so with one step of prefetch the loop waited a load latency
-    // per step (B = 8,192: 54 us for 0.9 GFLOP)
-    constexpr int kDepth = 8;
-    f32x4 ab[kDepth], wb[kDepth][4];
-    auto load_step = [&](int kt, f32x4& a, f32x4 (&w)[4]) __attribute__((always_inline)) {
+    // a ring of kDepth K-steps of operands in flight: one step's 4 MFMAs are far shorter than a
+    // global load (B = 8,192 with one wave per 64 columns and one step of prefetch: 54 us)
+    constexpr int kDepth = 16;
+    f32x4 ab[kDepth], wb[kDepth];
+    auto load_step = [&](int kt, f32x4& a, f32x4& w) __attribute__((always_inline)) {
         a = mv ? *(const f32x4*)(arow + 16 * kt) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = nv[j] ? *(const f32x4*)(wrow[j] + 16 * kt) : f32x4{0.f, 0.f, 0.f, 0.f};
+        w = nv ? *(const f32x4*)(wrow + 16 * kt) : f32x4{0.f, 0.f, 0.f, 0.f};
     };
 #pragma unroll
     for (int d = 0; d < kDepth; ++d)
@@ -457,15 +453,20 @@ __global__ __launch_bounds__(64) void conv_gemm_f32_narrow(ConvGemmParams p) {
             const int kt = kt0 + d;
             if (kt < nk) {
 #pragma unroll
-                for (int s = 0; s < 4; ++s)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ab[d][s], wb[d][j][s], acc[0][j], 0, 0, 0);
+                for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ab[d][s], wb[d][s], acc, 0, 0, 0);
                 if (kt + kDepth < nk) load_step(kt + kDepth, ab[d], wb[d]);
             }
         }
     }
-    epilogue_scalar<float, 1>(p, acc, m0, 0, lane);
+    // epilogue_scalar's mapping for this column block: column n, rows m0 + 4 c + q
+    if (nv) {
+        const float sc = p.scale[n], sh = p.shift[n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int mm = m0 + 4 * c + q;
+            if (mm < p.M) epi_store<float>(p, mm, n, acc[q], sc, sh);
+        }
+    }
 }
 
 // VP3D_F32_NARROW=0 (measurement; read at every launch): the tile kernel instead
@@ -504,7 +505,7 @@ hipError_t launch_conv_gemm(const ConvGemmParams& p, Act a_type, Act out_type, A
     if (compute == Act::F32) {
         if (a_type != Act::F32 || out_type != Act::F32) return hipErrorInvalidValue;
         if (f32_narrow_eligible(p)) {
-            hipLaunchKernelGGL(conv_gemm_f32_narrow, dim3((p.M + 15) / 16), dim3(64), 0, stream, p);
+            hipLaunchKernelGGL(conv_gemm_f32_narrow, dim3((p.M + 15) / 16), dim3(256), 0, stream, p);
             return hipGetLastError();
         }
         if ((p.Ktap % kF32Bk == 0) && (p.lda % 4 == 0) && aligned(p.A, 16))
