@@ -188,11 +188,13 @@ def test_a4_half_n_tail_bit_identical(dtype, monkeypatch):
     _check(ys["hn"][sel], ref, gt, dtype)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "f16x3"])
 def test_dilated_seq_a4_bit_identical_to_q64(dtype, monkeypatch):
     """VP3D_GEMM=a4 puts the dilated k3 convs of a long sequence (taps d rows apart: the tile's
     k offset steps d rows at every tap) on conv_gemm_a4; q64 sums in the same order.  40,000
-    frames: every block layer has >= 384 tiles of 256 x 256 (both kernels' threshold)."""
+    frames: every block layer has >= 384 tiles of 256 x 256 (both kernels' threshold), 2 rounds
+    + 112 tiles -- f16x3 runs those tails as half-N tiles (the k3 and the 1x1 + residual
+    layers, the residual rows offset by the dilation's crop)."""
     monkeypatch.setenv("VP3D_A4_SPLIT", "0")  # whole tiles only (a split-K last round sums in two chains)
     model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
     x = synth.normalized_windows(1, "x1_40000", 1, 40000)
