@@ -156,12 +156,17 @@ __device__ unsigned long long* g_a4_trace;
 // channels, accumulator blocks (i, j < 4), 8 A + 4 W LDS-DMA pieces per K-tile -- over the
 // M-tiles from p.sk_full on, one unit per workgroup (no walk, no split, no residual).  Every
 // output keeps the whole tile's K order, so the same bits as a 256 x 256 tile.
-template <typename CT, int ABL, int X3 = 0, bool GD = true, bool SPLIT = false, bool HN = false>
+// HNL = 2 (quarter-N, f16x3 only): 256 x 64 tiles, each wave 128 x 32, for tails of <= a
+// quarter round.
+template <typename CT, int ABL, int X3 = 0, bool GD = true, bool SPLIT = false, int HNL = 0>
 __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
+    constexpr bool HN = HNL > 0;
     static_assert(!HN || (GD && !SPLIT), "half-N tiles: grouped pieces, no split");
-    constexpr int TN = HN ? GN / 2 : GN;  // tile channels
-    constexpr int NJ = TN / 32;           // channel blocks of 16 per wave (two wave columns)
-    constexpr int WP = HN ? 4 : 8;        // W pieces per wave and K-tile
+    static_assert(HNL < 2 || X3 != 0, "quarter-N tiles: the split-fp16 epilogue only");
+    constexpr int TN = GN >> HNL;  // tile channels
+    constexpr int NJ = TN / 32;    // channel blocks of 16 per wave (two wave columns)
+    constexpr int WP = TN / 32;    // W pieces per wave and K-tile (TN rows x 128 B, 4 waves)
+    constexpr int NB = NJ < 4 ? NJ : 4;  // blocks of a 64-channel epilogue half
     // the accumulator file is this kernel's own from here on (see the header)
     asm volatile("" ::: A4_ALL_AGPRS);
     // a copy whose fields go through an empty asm every tile (below): values derived from them
@@ -272,7 +277,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int q = GD ? 8 * swv + i : swv + 4 * i;  // the piece's slot: rows 8q .. 8q + 7
-            const int qw = HN ? 4 * swv + (i & 3) : q;      // HN: 4 W slots per wave
+            const int qw = HN ? WP * swv + (i % WP) : q;   // HN: WP W slots per wave
             const int lci = GD ? (sln & 7) ^ (((i & 1) * 4 + (spr >> 1)) & 7) : lc;
             const int reb = GD ? kReb - (i & 3) * 1024 : 0;
             int m = m0 + 8 * q + spr;
@@ -301,7 +306,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
         int w = widu;
         launder_s(w);
         char* b = buf + 8 * w * 1024;
-        if constexpr (HN) return Bases{{b, b + 4096, buf + GW_OFF + 4 * w * 1024, nullptr}};
+        if constexpr (HN) return Bases{{b, b + 4096, buf + GW_OFF + WP * w * 1024, nullptr}};
         return Bases{{b, b + 4096, b + GW_OFF, b + GW_OFF + 4096}};
     };
     auto piece_lds = [&](char* buf, int i) __attribute__((always_inline)) -> char* {
@@ -409,12 +414,13 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             static_for<NJ>([&](auto j_c) __attribute__((always_inline)) {
                 constexpr int J = decltype(j_c)::value;
                 if constexpr (HN) {
-                    // 4 MFMAs per row block: A read, DMA piece I (A), W read (I < 4), piece 8 + I (W)
+                    // NJ MFMAs per row block: A read, DMA piece I (A), W read (I < NJ), piece 8 + I (W)
+                    constexpr int JWR = NJ > 2 ? 2 : 1;
                     if constexpr (DO_RD && J == 0) fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
                     if constexpr (DO_DMA && J == 1) dma_piece(dbuf, std::integral_constant<int, I>{}, s, aoff, bs);
-                    if constexpr (DO_RD && J == 2 && I < 4)
+                    if constexpr (DO_RD && J == JWR && I < NJ)
                         fw[NXT][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo);
-                    if constexpr (DO_DMA && J == 3 && I < 4)
+                    if constexpr (DO_DMA && J == NJ - 1 && I < WP)
                         dma_piece(dbuf, std::integral_constant<int, 8 + I>{}, s, aoff, bs);
                 } else {
                     if constexpr (DO_RD && J == 0) fa[NXT][I] = *(const u32x4*)(rbuf + a_base + I * 2048 + fo);
@@ -628,7 +634,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
             if (nk > 1)
             {
                 if constexpr (HN)
-                    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // K-tile 0 landed (younger: K-tile 1)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + WP) : "memory");  // K-tile 0 landed (younger: K-tile 1)
                 else
                     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
             }
@@ -656,7 +662,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             fa[0][i] = *(const u32x4*)(buf0 + a_base + i * 2048 + fo0);
-            if (!HN || i < 4) fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
+            if (i < NJ) fw[0][i] = *(const u32x4*)(buf0 + w_base + i * 2048 + fo0);
         }
         if constexpr (X3 != 0) {
             // ---- split fp16 (VP3D_DTYPE_F16X3): rows hold every f32 value as f16 halves, each
@@ -718,11 +724,12 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 constexpr bool DO_DMA = decltype(dma_c)::value && !(ABL & 1);
                 const int64_t aoff = DO_DMA ? a_koff(s) : 0;
                 const Bases bs = DO_DMA ? bases_of(dbuf) : Bases{};
-                // (HN: 4 channel blocks; the W reads / pieces move from J = 4 / 2 to 2 / 3, I < 4)
-                constexpr int JW = HN ? 2 : 4;
+                // (HN: NJ channel blocks; the W reads / pieces move from J = 4 / 2 to 2 / 3 (1 / 1
+                // for NJ = 2), I < NJ)
+                constexpr int JW = HN ? (NJ > 2 ? 2 : 1) : 4;
                 static_for<8>([&](auto i_c) __attribute__((always_inline)) {
                     constexpr int I = decltype(i_c)::value;
-                    constexpr bool WI = !HN || I < 4;  // a W block to read / a W piece to issue
+                    constexpr bool WI = !HN || I < NJ;  // a W block to read / a W piece to issue
                     static_for<NJ>([&](auto j_c) __attribute__((always_inline)) {
                         constexpr int J = decltype(j_c)::value;
                         if constexpr (KIND == 0) {
@@ -743,7 +750,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                                 fa[1 - H][7] = *(const u32x4*)(rbuf + a_base + 7 * 2048 + fo0);
                             if constexpr (DO_RD && J == JW && WI)
                                 fw[0][I] = *(const u32x4*)(rbuf + w_base + I * 2048 + fo0);
-                            if constexpr (DO_DMA && J == (HN ? 3 : 2) && WI)
+                            if constexpr (DO_DMA && J == (HN ? NJ - 1 : 2) && WI)
                                 dma_piece(dbuf, std::integral_constant<int, 8 + I>{}, s, aoff, bs);
                             if constexpr (RQ >= 0 && !HN && (J == 2 || J == 6))
                                 xres_piece(rqbuf, i_c, std::integral_constant<int, J / 4>{}, RQ, 0);
@@ -869,7 +876,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                 const int nw = en0 + ewc * (TN / 2) + 64 * HH;
                 f32x2 sc[4][2], sh[4][2];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < NB; ++j) {
                     const int n = nw + 16 * j + 4 * egrp;
                     const f32x4 s4 = *(const f32x4*)&s_scale[n];
                     const f32x4 h4 = *(const f32x4*)&s_shift[n];
@@ -882,7 +889,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                     constexpr int I = decltype(i_c)::value;
                     const int m = em0 + ewr * 128 + 16 * I + er16;
                     float v4[4][4];  // [block j][element]: BN + ReLU, accumulator layout
-                    static_for<4>([&](auto j_c) __attribute__((always_inline)) {
+                    static_for<NB>([&](auto j_c) __attribute__((always_inline)) {
                         constexpr int J = decltype(j_c)::value;
                         constexpr int R = 4 * (8 * I + 4 * HH + J);
                         f32x2 v[2] = {f32x2{aread<R>(), aread<R + 1>()}, f32x2{aread<R + 2>(), aread<R + 3>()}};
@@ -901,7 +908,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                         }
                     });
 #pragma unroll
-                    for (int jp = 0; jp < 2; ++jp) {
+                    for (int jp = 0; jp < NB / 2; ++jp) {
                         float* x = v4[2 * jp];
                         float* y = v4[2 * jp + 1];
                         asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\t"
@@ -1028,7 +1035,7 @@ __global__ __launch_bounds__(256, 1) void conv_gemm_a4(ConvGemmParams p_arg) {
                             m = m < p.M ? m : p.M - 1;  // valid address; rows past M are never stored
                             const int off = ((res_row(p, m) - rrow0) * p.ldr + 2 * nw + ec0) * 2;
 #pragma unroll
-                            for (int jp = 0; jp < 2; ++jp) {
+                            for (int jp = 0; jp < NB / 2; ++jp) {  // (quarter-N: the wave's 32 channels only)
                                 rr[i][jp][0] = __builtin_bit_cast(
                                     u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx_rsrc, off + 128 * jp, 0, 0));
                                 rr[i][jp][1] = __builtin_bit_cast(
@@ -1198,7 +1205,7 @@ bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
     return (size_t)p.N * p.Kp < (1u << 31);
 }
 
-static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3);
+static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3, int* level = nullptr);
 
 bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32) {
     if (p.Ktap % GK != 0 || p.Kp % GK != 0 || p.lda % 8 != 0) return false;
@@ -1268,9 +1275,12 @@ static void a4_split_plan(ConvGemmParams& q, int ntiles, int nk, bool need_ws = 
 // 16-bit operands only where the layer has no whole round (block 4 at 8,192: 0.060 vs 0.085
 // ms; 1,024 windows +8 %) -- after whole rounds their half tiles, DMA-issue-bound at 12 pieces
 // per 64 MFMAs, ran no faster than the whole-tile round (block 3 at 8,192: 0.157 vs 0.148).
-// VP3D_A4_HN=0 (measurement) turns it off; VP3D_A4_SPLIT=2 (the split-K test) takes
-// precedence.  Returns the M-tiles of the tail (0: none).
-static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3) {
+// f16x3 tails of <= a quarter round run as 4L quarter-N tiles of 256 x 64 (level 2): sequence
+// mode's 4-tile tails and config 4 at 1,024 windows (blocks 3, 4), +1 % / +3.4 % same box
+// (profiles/r05_a4_quarter_n_tail_ab.txt).  VP3D_A4_HN=0 (measurement) turns it off, 1 keeps
+// half tiles only; VP3D_A4_SPLIT=2 (the split-K test) takes precedence.  Returns the M-tiles
+// of the tail (0: none) and in *level 1 (half-N) or 2 (quarter-N).
+static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3, int* level) {
     const char* e = getenv("VP3D_A4_HN");
     if (e && e[0] == '0') return 0;
     const char* sp = getenv("VP3D_A4_SPLIT");
@@ -1281,6 +1291,8 @@ static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3) {
     if ((p.R != nullptr && !x3) || ncu <= 0 || ntn <= 0) return 0;
     const int L = ntiles % ncu;
     if (L == 0 || 2 * L > ncu || L % ntn != 0 || (!x3 && ntiles >= ncu)) return 0;
+    // f16x3 tails of <= a quarter round: 4L quarter-N units of 256 x 64 (VP3D_A4_HN=1: half only)
+    if (level) *level = x3 && 4 * L <= ncu && !(e && e[0] == '1') ? 2 : 1;
     return L / ntn;
 }
 
@@ -1312,7 +1324,7 @@ static void a4_launch(const ConvGemmParams& p, dim3 grid, bool split, hipStream_
 // the whole rounds (M-tiles below ntm - mt_tail, if any; walked by one workgroup per CU when
 // `walk_cus` > 0) then the tail as half-N units
 template <typename CT, int X3>
-static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t stream, int walk_cus = 0) {
+static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t stream, int walk_cus = 0, int level = 1) {
     const int ntm = (p.M + GM - 1) / GM;
     const int mt0 = ntm - mt_tail;
     if (mt0 > 0) {
@@ -1326,7 +1338,14 @@ static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t strea
     ConvGemmParams t = p;
     t.sk_split = t.sk_left = 0;
     t.sk_full = mt0;  // the HN launch's first M-tile
-    hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false, true>), dim3(mt_tail * (p.N / (GN / 2))), dim3(256), 0,
+    if constexpr (X3 != 0) {
+        if (level == 2) {
+            hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false, 2>), dim3(mt_tail * (p.N / (GN / 4))), dim3(256),
+                               0, stream, t);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false, 1>), dim3(mt_tail * (p.N / (GN / 2))), dim3(256), 0,
                        stream, t);
 }
 
@@ -1346,15 +1365,16 @@ hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p_in, bool out_f32, hipS
     ConvGemmParams p = p_in;
     const char* we = getenv("VP3D_A4_WALK");
     const int walk_mode = we ? atoi(we) : 1;
-    const int hn_tail = walk_mode == 2 ? 0 : a4_hn_tail(p, ntiles, true);
+    int hn_level = 1;
+    const int hn_tail = walk_mode == 2 ? 0 : a4_hn_tail(p, ntiles, true, &hn_level);
 #ifndef VP3D_ABLATION
     if (hn_tail > 0) {
         // the whole rounds walked as without the tail (the 1x1 + residual layers)
         const int wc = walk_mode > 0 && p.R != nullptr ? a4_cus() : 0;
         if (out_f32)
-            a4_launch_hn<_Float16, 2>(p, hn_tail, stream, wc);
+            a4_launch_hn<_Float16, 2>(p, hn_tail, stream, wc, hn_level);
         else
-            a4_launch_hn<_Float16, 1>(p, hn_tail, stream, wc);
+            a4_launch_hn<_Float16, 1>(p, hn_tail, stream, wc, hn_level);
         return hipGetLastError();
     }
 #endif

@@ -161,14 +161,15 @@ def test_gemm_a4_bit_identical_to_q64(dtype, walk, monkeypatch):
     _check(ys["a4"][sel], ref, gt, dtype)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "f16x3"])
-def test_a4_half_n_tail_bit_identical(dtype, monkeypatch):
+@pytest.mark.parametrize("dtype,B", [("bf16", 8192), ("f16x3", 8192), ("f16x3", 1024)])
+def test_a4_half_n_tail_bit_identical(dtype, B, monkeypatch):
     """B = 8,192: every block conv leaves 128 tiles past its whole rounds (block 4: 128 tiles in
     all); the k3 convs run them as 256 half-N tiles of 256 x 128 (conv_gemm_a4 HN, a second
     launch) -- the same bits as q64's whole tiles and as a4's own whole tiles (VP3D_A4_HN=0,
-    no split-K)."""
+    no split-K).  B = 1,024, f16x3: blocks 3 and 4 (48 / 16 tiles) run as quarter-N tiles of
+    256 x 64."""
     model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
-    x = synth.normalized_windows(1, "x8192_243", 8192, 243)
+    x = synth.normalized_windows(1, f"x{B}_243", B, 243)
     model.cuda().set_compute_dtype(dtype)
     xd = torch.from_numpy(x).cuda()
     ys = {}
@@ -182,7 +183,7 @@ def test_a4_half_n_tail_bit_identical(dtype, monkeypatch):
     assert np.isfinite(ys["hn"]).all()
     assert np.array_equal(ys["hn"], ys["whole"]), np.abs(ys["hn"] - ys["whole"]).max()
     assert np.array_equal(ys["hn"], ys["q64"]), np.abs(ys["hn"] - ys["q64"]).max()
-    sel = np.r_[0:32, 8160:8192]
+    sel = np.r_[0:32, B - 32:B]
     ref = lifter_forward(sd, x[sel], [3, 3, 3, 3, 3], causal=False, strided=True, dense=False).numpy()
     gt = synth.gt_poses(3, "gt", 64, 17).reshape(ref.shape)
     _check(ys["hn"][sel], ref, gt, dtype)
@@ -199,6 +200,23 @@ def test_dilated_seq_a4_bit_identical_to_q64(dtype, monkeypatch):
     model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
     x = synth.normalized_windows(1, "x1_40000", 1, 40000)
     model.cuda().set_compute_dtype(dtype)
+    xd = torch.from_numpy(x).cuda()
+    ys = {}
+    for gemm in ("q64", "a4"):
+        monkeypatch.setenv("VP3D_GEMM", gemm)
+        with torch.no_grad():
+            ys[gemm] = model(xd).cpu().numpy()
+    assert np.isfinite(ys["a4"]).all()
+    assert np.array_equal(ys["a4"], ys["q64"]), np.abs(ys["a4"] - ys["q64"]).max()
+
+
+def test_dilated_seq_quarter_n_tail_bit_identical(monkeypatch):
+    """Sequence mode at the bench's length (65,778 frames in, 65,536 poses): every block layer
+    is 4 rounds + 4 tiles, which f16x3 runs as 16 quarter-N tiles of 256 x 64 (k3 and 1x1 +
+    residual, dilated taps) -- the same bits as q64."""
+    model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
+    x = synth.normalized_windows(1, "x1_65778", 1, 65778)
+    model.cuda().set_compute_dtype("f16x3")
     xd = torch.from_numpy(x).cuda()
     ys = {}
     for gemm in ("q64", "a4"):
