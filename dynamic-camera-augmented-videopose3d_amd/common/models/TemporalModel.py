@@ -133,7 +133,8 @@ class TemporalModelBase(nn.Module):
         return total
 
     def set_compute_dtype(self, dtype):
-        """'fp32' (default, parity path), 'bf16' or 'fp16'."""
+        """'fp32' (default, parity path), 'f16x3' (split fp16: fp32-level results on the 16-bit
+        MFMAs), 'bf16' or 'fp16'."""
         if dtype not in _N.DTYPES:
             raise ValueError(f"unknown compute dtype {dtype!r}")
         self.compute_dtype = dtype
