@@ -222,7 +222,7 @@ def stream_main(args, world, rank, dev, emit=True):
     cpu = getattr(args, "stream_cpu_baseline", None)
     if cpu is None and args.cpu_seconds > 0:
         win = xp[:, :RF_FULL].contiguous()
-        cpu = cpu_baseline(lambda: lifter_forward(sd, win, FW, causal=True), 1, "poses/s",
+        cpu = cpu_baseline(cpu_job("lifter", sd, {"x": win}, fw=FW, causal=True), 1, "poses/s",
                            "single-frame causal steps (one 243-frame window through the torch-CPU "
                            "restatement each, B = 1)", target_s=args.cpu_seconds / 5)
     out = {
@@ -276,6 +276,7 @@ def stream_main(args, world, rank, dev, emit=True):
                              if serve_lat else None),
         "serve_python_latency_us": round(float(np.median(serve_py)), 2) if serve_py else None,
         "eager_step_latency_us": round(float(np.median(lat)), 2),
+        "faults": 0,  # st.check() after the timed graphs and after the parity steps
         "parity": {"frames": T, f"{args.dtype}_max_coord_delta_mm": float(np.abs(outs - ref).max()) * 1e3,
                    f"{args.dtype}_mpjpe_delta_mm": abs(mp(outs) - mp(ref)) * 1e3,
                    "meets_north_star_1e-4mm": bool(abs(mp(outs) - mp(ref)) * 1e3 <= 1e-4),
@@ -286,7 +287,7 @@ def stream_main(args, world, rank, dev, emit=True):
         out["speedup_vs_cpu"] = round(out["value"] / cpu["value"], 1)
     st.close()
     if emit:
-        print(json.dumps(out), flush=True)
+        emit_line(out)
     return out
 
 
@@ -392,16 +393,14 @@ def train_main(args, world, rank, dev):
         "loss_last": float(loss.item()),
     }
     if args.cpu_seconds > 0:
-        from oracle.train_ref import TrainLoop
-        loop = TrainLoop(sd, FW, lr=1e-3, amsgrad=True)
         rng = np.random.default_rng(0)
         xb = (rng.standard_normal((8, RF, JOINTS, 2)) * 0.3).astype(np.float32)
         tb = (rng.standard_normal((8, 1, JOINTS, 3)) * 0.2).astype(np.float32)
-        out["cpu_baseline"] = cpu_baseline(lambda: loop.step(xb, tb), 8, "windows/s",
+        out["cpu_baseline"] = cpu_baseline(cpu_job("train", sd, {"x": xb, "tgt": tb}, fw=FW), 8, "windows/s",
                                            "training iterations on batches of 8 windows (dropout 0) through "
                                            "oracle/train_ref.py (torch-CPU autograd + Adam)",
                                            target_s=args.cpu_seconds / 5)
-    print(json.dumps(out), flush=True)
+    emit_line(out)
 
 
 def seq_flop_per_pose(kind, W=243, d=128, layers=2, ff=128, heads=4, head=(128, 128, 128), cin=46, jout=51,
@@ -485,16 +484,13 @@ def seq_main(args, world, rank, dev):
         "flop_per_pose": flop, "tflops_effective": round(poses_s * flop / 1e12, 3),
     }
     if args.cpu_seconds > 0:
-        from oracle.seq_lifter_ref import lstm_forward, sliding_windows, transformer_forward
+        from oracle.seq_lifter_ref import sliding_windows
         w2, wc = sliding_windows(x2[:, :64 + W - 1].cpu(), xc[:, :64 + W - 1].cpu(), W)
-        if kind == "transformer":
-            fn = lambda: transformer_forward(sd, w2, wc, 4, 2, 3)  # noqa: E731
-        else:
-            fn = lambda: lstm_forward(sd, w2, wc, 128, 2, 3)  # noqa: E731
+        fn = cpu_job(kind, sd, {"x": w2, "xc": wc})
         out["cpu_baseline"] = cpu_baseline(fn, 64, "poses/s", "64 sliding windows per run through "
                                            "oracle/seq_lifter_ref.py (torch-CPU, the reference's op sequence)",
                                            target_s=args.cpu_seconds / 5)
-    print(json.dumps(out), flush=True)
+    emit_line(out)
 
 
 class SequenceCase:
@@ -525,7 +521,9 @@ class SequenceCase:
         def step():
             lifter.forward(x, dtype, out=y)
         with torch.no_grad():
-            return profiled_run(lifter, step, steps, warmup, settle_s, world)
+            r = profiled_run(lifter, step, steps, warmup, settle_s, world)
+        lifter.sync_status()  # raises on a device-side fault of any forward of the leg
+        return r
 
     def parity(self, P=256):
         """The first P output frames (a time shard: inputs [0, P + RF - 1)) vs the oracle."""
@@ -554,14 +552,12 @@ class SequenceCase:
         return dt, {"value": round(value, 2), "unit": "poses/s", "steps": steps,
                     "ms_per_step": round(dt / steps * 1e3, 4),
                     "tflops_effective": round(value / self.T_out * self.flop_step / 1e12, 2),
-                    "roofline": r, "per_layer_ms": per_layer, **self.parity()}
+                    "roofline": r, "per_layer_ms": per_layer, "faults": 0, **self.parity()}
 
     def cpu_baseline(self, seconds):
-        from oracle.temporal_ref import lifter_forward
         Tc = 2048
         xc = self.x[:, :Tc + self.RF - 1].cpu()
-        sd = self.sd
-        return cpu_baseline(lambda: lifter_forward(sd, xc, FW), Tc, "poses/s",
+        return cpu_baseline(cpu_job("lifter", self.sd, {"x": xc}, fw=FW), Tc, "poses/s",
                             f"one sequence of {Tc + self.RF - 1} frames -> {Tc} poses per run through "
                             "oracle/temporal_ref.py (torch-CPU, fp32)", target_s=seconds / 5)
 
@@ -593,6 +589,7 @@ def sequence_main(args, world, rank, dev):
                    "parallelism": f"dp{world} (independent sequences)"},
         "flop_per_step": case.flop_step, "tflops_effective": round(value / T_out * case.flop_step / 1e12, 2),
         "roofline": leg["roofline"], "per_layer_ms": leg["per_layer_ms"],
+        "faults": leg["faults"],
         "parity": {k: leg[k] for k in ("frames_checked", "mpjpe_delta_mm", "max_coord_delta_mm",
                                        "meets_north_star_1e-4mm")},
     }
@@ -600,7 +597,20 @@ def sequence_main(args, world, rank, dev):
         out["cpu_baseline"] = case.cpu_baseline(args.cpu_seconds)
         out["speedup_vs_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
     case.close()
-    print(json.dumps(out), flush=True)
+    emit_line(out)
+
+
+# keys the driver must see: it keeps only the TAIL of stdout, so the headline's own timing,
+# roofline, CPU baseline, fault count and parity go last, after the (long) legs
+TAIL_KEYS = ("per_layer_ms", "per_layer_note", "tflops_effective", "roofline", "cpu_baseline", "speedup_vs_cpu",
+             "faults", "faults_note", "parity")
+
+
+def emit_line(out):
+    """Print the ONE JSON line of this run, the contract fields first and TAIL_KEYS last."""
+    head = {k: v for k, v in out.items() if k not in TAIL_KEYS}
+    head.update({k: out[k] for k in TAIL_KEYS if k in out})
+    print(json.dumps(head), flush=True)
 
 
 def host_cpu_info():
@@ -626,7 +636,7 @@ def host_cpu_info():
 
 
 def cpu_threads():
-    """Threads for the CPU baseline: all physical cores of this host, capped by the CPU share
+    """Threads for the CPU baseline: one per physical core of this host, capped by the CPU share
     the job was given (OMP_NUM_THREADS: 16 per GPU on the MI355X boxes)."""
     info = host_cpu_info()
     n = info["host_physical_cores"] or os.cpu_count() or 1
@@ -636,57 +646,93 @@ def cpu_threads():
     return n, info
 
 
-def cpu_baseline(run_once, units_per_run, unit, sample_desc, repeats=5, target_s=2.5):
-    """Median of `repeats` timed runs (after one warm-up) of the oracle on the host cores.
-    run_once() processes `units_per_run` units; each timed run repeats it to ~target_s."""
-    threads, info = cpu_threads()
-    prev = torch.get_num_threads()
-    torch.set_num_threads(threads)
+def cpu_job(kind, sd, arrays, **kwargs):
+    """A CPU-baseline job for oracle/cpu_timer.py: the oracle function `kind` on `arrays` with
+    the state dict `sd` (numpy or torch values)."""
+    return {"kind": kind, "sd": sd, "arrays": arrays, "kwargs": kwargs}
+
+
+def _timer_child(job, units, cpus, target_s, repeats):
+    """Run oracle/cpu_timer.py on `job` in a child process pinned one thread per CPU of `cpus`
+    (this process keeps the GPU; the child never touches it).  Returns its JSON record."""
+    import shutil
+    import subprocess
+    import tempfile
+    from oracle.cpu_timer import child_env
+
+    def host(v):
+        return v.detach().to("cpu").numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+    tmp = tempfile.mkdtemp(prefix="vp3d_cpu_")
     try:
-        run_once()  # warm-up (thread pool spin-up, allocator)
-        # the repeat count from a second, warm run: calibrating on the cold first run left
-        # the timed runs ~40 % short of target_s
-        t = time.perf_counter()
-        run_once()
-        t1 = max(time.perf_counter() - t, 1e-3)
-        reps = max(1, int(round(target_s / t1)))
-        rates = []
-        for _ in range(repeats):
-            t = time.perf_counter()
-            for _ in range(reps):
-                run_once()
-            rates.append(reps * units_per_run / (time.perf_counter() - t))
+        path = os.path.join(tmp, "job.npz")
+        meta = {"kind": job["kind"], "kwargs": job["kwargs"], "units": int(units), "target_s": float(target_s),
+                "repeats": int(repeats), "threads": len(cpus)}
+        payload = {f"sd:{k}": np.ascontiguousarray(host(v)) for k, v in job["sd"].items()}
+        payload.update({k: np.ascontiguousarray(host(v)) for k, v in job["arrays"].items()})
+        np.savez(path, meta=np.array(json.dumps(meta)), **payload)
+        r = subprocess.run([sys.executable, "-m", "oracle.cpu_timer", path], cwd=REPO, env=child_env(cpus),
+                           capture_output=True, text=True, timeout=max(300.0, 6 * target_s * (repeats + 2)))
     finally:
-        torch.set_num_threads(prev)
+        shutil.rmtree(tmp, ignore_errors=True)
+    if r.returncode != 0 or not r.stdout.strip():
+        raise RuntimeError(f"cpu baseline child failed (rc {r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def cpu_baseline(job, units_per_run, unit, sample_desc, repeats=5, target_s=2.5, all_cores=False):
+    """Median of `repeats` timed runs (after a warm-up and a calibration run) of the oracle on
+    the host cores, in a child process whose torch threads are pinned one per distinct physical
+    core inside this process's affinity set (OMP_PLACES / OMP_PROC_BIND; oracle/cpu_timer.py).
+    One run of `job` processes `units_per_run` units; each timed run repeats it to ~target_s.
+    all_cores: also one short timing on every physical core of the affinity set (side figure)."""
+    from oracle.cpu_timer import cgroup_cpu_quota, pick_cores
+    threads, info = cpu_threads()
+    cpus, n_phys = pick_cores(threads)
+    res = _timer_child(job, units_per_run, cpus, target_s, repeats)
     try:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = None
-    return {"value": round(float(np.median(rates)), 3), "unit": unit, "cores": threads, "kind": "port",
-            "affinity_cpus": affinity,
-            "sample": f"{sample_desc}; median of {repeats} runs of {reps} x {units_per_run} after 2 warm-ups "
-                      f"({sum(reps * units_per_run / r for r in rates):.1f} s timed)",
-            "runs": [round(r, 3) for r in rates], "runs_order": "time order", **info,
-            "threads_note": "torch threads = host physical cores capped by the job's CPU share (OMP_NUM_THREADS)"}
+    pinned = [t for t in res["thread_cpu_map"] if "," not in t["allowed"] and "-" not in t["allowed"]]
+    out = {"value": res["value"], "unit": unit, "cores": len(cpus), "kind": "port",
+           "sample": f"{sample_desc}; median of {repeats} runs of {res['reps']} x {units_per_run} after a warm-up "
+                     f"and a calibration run ({res['timed_s']:.1f} s timed)",
+           "runs": res["runs"], "runs_order": "time order", "spread": res["spread"],
+           "pinned_cpus": cpus, "threads_pinned": len(pinned),
+           "pinned_threads_ran_on": sorted({t["last_cpu"] for t in pinned}),
+           "affinity_cpus": affinity, "affinity_physical_cores": n_phys, "cgroup_cpu_quota": cgroup_cpu_quota(),
+           **info,
+           "threads_note": "torch threads = physical cores capped by the job's CPU share (OMP_NUM_THREADS), one "
+                           "thread pinned per distinct physical core (first logical CPU of each core in "
+                           "sched_getaffinity; OMP_PLACES + OMP_PROC_BIND=close in a child process)"}
+    if all_cores and n_phys > len(cpus):
+        allc, _ = pick_cores(None)
+        r2 = _timer_child(job, units_per_run, allc, max(0.6, target_s / 3), 3)
+        out["all_physical_cores"] = {"value": r2["value"], "cores": len(allc), "runs": r2["runs"],
+                                     "spread": r2["spread"],
+                                     "note": "side figure: one thread per physical core of the whole affinity "
+                                             "set, beyond the job's CPU share (other jobs may share these cores)"}
+    return out
 
 
-def timed_steps(step, steps, warmup, settle_s, world):
+def timed_steps(step, steps, warmup, settle_s, world, sync=None):
     """W warm-up steps, untimed steps until the device has run `settle_s` (clock ramp),
     then exactly `steps` steps bracketed by barrier + synchronize; returns seconds."""
+    sync = sync or torch.cuda.synchronize
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     t = time.perf_counter()
     while time.perf_counter() - t < settle_s:
         step()
-        torch.cuda.synchronize()
+        sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     return time.perf_counter() - t0
@@ -821,6 +867,8 @@ class WindowsCase:
         with torch.no_grad():
             dt, per_layer, dom = profiled_run(self.lifter, self.make_step(dtype, y, x=self.x), steps, warmup,
                                               settle_s, world)
+        # a device-side fault of any forward of the leg (split-K timeout, f16x3 range) raises here
+        self.lifter.sync_status()
         return dt, per_layer, dom, y
 
     def parity_ref(self, P):
@@ -863,14 +911,12 @@ class WindowsCase:
                 "reference_fp32_vs_fp64_max_coord_delta_mm": float(np.abs(ref - ref64).max()) * 1e3,
                 "output_rms_m": round(float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))), 6)}
 
-    def cpu_baseline(self, seconds):
-        from oracle.temporal_ref import lifter_forward
+    def cpu_baseline(self, seconds, all_cores=False):
         xc = self.pool.seqs.gather(self.pairs[:64].contiguous(), self.RF, self.pad, "2d",
                                    concat_cams=self.traj).view(-1, self.RF, self.jin, 2).cpu()
-        sd = self.sd
-        return cpu_baseline(lambda: lifter_forward(sd, xc, FW, strided=True), int(xc.shape[0]), "poses/s",
-                            f"windows of 243x{self.jin}x2 through oracle/temporal_ref.py (torch-CPU, fp32, batch "
-                            f"{int(xc.shape[0])})", target_s=seconds / 5)
+        return cpu_baseline(cpu_job("lifter", self.sd, {"x": xc}, fw=FW, strided=True), int(xc.shape[0]),
+                            "poses/s", f"windows of 243x{self.jin}x2 through oracle/temporal_ref.py (torch-CPU, fp32, "
+                            f"batch {int(xc.shape[0])})", target_s=seconds / 5, all_cores=all_cores)
 
     def leg(self, dtype, steps, warmup, settle_s, P, G=None):
         """One dtype on this case (rank 0, N = 1): rate, roofline, per-layer times, parity."""
@@ -880,7 +926,7 @@ class WindowsCase:
                "ms_per_step": round(dt / steps * 1e3, 4),
                "tflops_effective": round((G or self.G) * steps / dt * self.flop_pose / 1e12, 2),
                "roofline": roofline_of(dom, PEAK_TFLOPS[dtype], traffic, tnote), "per_layer_ms": per_layer,
-               **self.parity(y, P)}
+               "faults": 0, **self.parity(y, P)}
         if dtype == "f16x3":
             out["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per algorithmic "
                                             "multiply-add (hi.hi + hi.lo + lo.hi)")
@@ -940,13 +986,16 @@ def windows_main(args, world, rank, dev):
         "roofline": roofline_of(dom, PEAK_TFLOPS[dtype], traffic, tnote),
         "per_layer_ms": per_layer,
         "per_layer_note": "untimed pass with HIP events around every launch",
+        "faults": 0,
+        "faults_note": "vp3d_sync_status after every timed leg: a device-side fault (split-K timeout, f16x3 "
+                       "range) raises instead of reporting",
         "parity": parity,
     }
     if dtype == "f16x3":
         out["roofline"]["peak_note"] = ("f16 dense MFMA peak / 3: three f16 products per algorithmic "
                                         "multiply-add (hi.hi + hi.lo + lo.hi)")
     if world > 1 or args.no_extras:
-        print(json.dumps(out), flush=True)
+        emit_line(out)
         return
     legs = ["bf16", "fp32"] if not traj else ["f16x3", "fp32"]
     for dl in legs:
@@ -976,13 +1025,14 @@ def windows_main(args, world, rank, dev):
                 ks = max(5, args.steps // 2)
                 with torch.no_grad():
                     dts = timed_steps(case.make_step(sdt, ysw, ps, xsw), ks, 3, 0.2, 1)
+                case.lifter.sync_status()
                 row[str(Bs)] = round(Bs * ks / dts, 2)
                 del ysw, xsw
             sweep[sdt] = row
         out["batch_sweep_poses_per_s"] = sweep
     # ---- CPU baseline: the oracle (reference op sequence) on 64 windows of the same set ----
     if args.cpu_seconds > 0:
-        cpu = case.cpu_baseline(args.cpu_seconds)
+        cpu = case.cpu_baseline(args.cpu_seconds, all_cores=True)
         out["cpu_baseline"] = cpu
         out["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         for dl in legs:
@@ -1032,14 +1082,89 @@ def windows_main(args, world, rank, dev):
                 a5.stream_cpu_baseline = c5["fp32"].get("cpu_baseline")
             c5[d5] = stream_main(a5, 1, 0, dev, emit=False)
         out["config5"] = c5
-    print(json.dumps(out), flush=True)
+    emit_line(out)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a CHILD process and
+    return its exit code.  This process never touches the GPU (device_count() does not
+    initialise it on this image); it refuses when fewer than N GPUs are visible, unless the
+    run is a rehearsal (VP3D_BENCH_REHEARSE=1: ranks share the GPUs; VP3D_BENCH_DRY=1: no GPU)."""
+    import subprocess
+    rehearse = os.environ.get("VP3D_BENCH_REHEARSE") == "1" or os.environ.get("VP3D_BENCH_DRY") == "1"
+    if not rehearse:
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {ndev} (VP3D_BENCH_REHEARSE=1 shares "
+                  "them for a rehearsal)", file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def dry_main(args, world, rank):
+    """VP3D_BENCH_DRY=1 (CPU tests only, never a reported number): the rank plumbing of the
+    default line -- the launcher, gloo rendezvous, this rank's shard_range of the global batch,
+    barrier-bracketed timing of K steps, MAX over ranks, ONE line from rank 0 -- with a CPU
+    stand-in step instead of the GPU forward."""
+    from vp3d_amd.shard import shard_range
+    if world > 1:
+        dist.init_process_group("gloo")
+    s, e = shard_range(args.global_batch, rank, world)
+    a = np.ones((64, 64), np.float32)
+
+    def step():
+        a.dot(a)
+    dt = timed_steps(step, args.steps, args.warmup, 0.0, world, sync=lambda: None)
+    t = torch.tensor([dt], dtype=torch.float64)
+    sizes = torch.tensor([e - s], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sizes, op=dist.ReduceOp.SUM)
+    dt = float(t.item())
+    if rank == 0:
+        emit_line({"metric": METRIC, "value": round(args.global_batch * args.steps / dt, 2), "unit": "poses/s",
+                   "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                   "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+                   "vs_baseline": None, "dtype": "none", "dry_run": True,
+                   "data": "DRY RUN (VP3D_BENCH_DRY=1): CPU stand-in step, rank plumbing only -- not a measurement",
+                   "config": {"workload": "dry rehearsal of the config-4 rank plumbing", "global_batch": args.global_batch,
+                              "windows_per_gpu": e - s, "windows_all_ranks": int(sizes.item()),
+                              "parallelism": f"dp{world} (contiguous shards, no collective)"}})
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # not under a launcher: start the N ranks ourselves (before any GPU call)
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to label a {world}-rank run as "
+              f"{args.gpus} GPUs", file=sys.stderr, flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("VP3D_BENCH_DRY") == "1":
+        dry_main(args, world, rank)
+        return
     # VP3D_BENCH_REHEARSE=1: rehearse the N-rank path on a box with fewer GPUs (ranks share
     # devices round-robin, gloo instead of RCCL); never used for reported numbers
     rehearse = os.environ.get("VP3D_BENCH_REHEARSE") == "1"

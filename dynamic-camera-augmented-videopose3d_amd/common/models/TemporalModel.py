@@ -169,6 +169,16 @@ class TemporalModelBase(nn.Module):
         self._lifter_key = key
         return self._lifter
 
+    def sync_status(self):
+        """Synchronise and raise RuntimeError if an eval-mode forward of this module reported a
+        device-side fault that has not been raised yet (NativeLifter.sync_status: a split-K
+        timeout, or an f16x3 activation past the f16 range / non-finite poses).  A forward
+        raises a pending fault of an EARLIER forward at entry; the last forward of a run is
+        only checked here (vp3d_amd.evaluate.evaluate calls it after its loop).  No-op
+        before the first eval-mode forward."""
+        if self._lifter is not None:
+            self._lifter.sync_status()
+
     def native_trainer(self, device) -> NativeTrainer:
         """The NativeTrainer (train-mode forward/backward engine) for `device`."""
         device = torch.device(device)
@@ -179,6 +189,10 @@ class TemporalModelBase(nn.Module):
         return self._trainer
 
     def forward(self, x):
+        """TemporalModel.py:62-76.  Eval mode runs libvp3d (compute dtype: set_compute_dtype);
+        a device-side fault of an EARLIER eval forward (split-K timeout; f16x3 range, which
+        blocks only f16x3 forwards) raises RuntimeError here, and one of the last forward is
+        raised by sync_status() -- call it before trusting a run's final outputs."""
         assert len(x.shape) == 4
         assert x.shape[-2] == self.num_joints_in
         assert x.shape[-1] == self.in_features

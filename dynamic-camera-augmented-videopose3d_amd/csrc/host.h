@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/vp3d.h"
+#include "kernels.h"  // vp3d::SplitCtl (the handle stages its control block)
 
 namespace vp3d {
 namespace host {
@@ -119,9 +120,11 @@ struct vp3d_handle {
     unsigned* sk_err_host = nullptr;
     unsigned* sk_err_dev = nullptr;
     // the split-K control block last written to the device (vp3d::SplitCtl: wait bound, fault
-    // word, fault injection), rewritten when the environment knobs change
+    // word, fault injection), written with the workspace and rewritten when the test knobs
+    // change; sk_ctl_stage is the host source of that async copy (per handle: no shared static)
     unsigned long long sk_ctl_spin = 0;
     int sk_ctl_drop = -1;
+    vp3d::SplitCtl sk_ctl_stage{};
     // profiling
     bool profiling = false;
     uint64_t prof_mask = ~0ull;  // layers timed while profiling (bit i = layer i)

@@ -203,17 +203,26 @@ hipError_t launch_pose_metrics(const float* pred, const float* target, int64_t n
 
 namespace vp3d {
 namespace {
-// any non-finite value of y[0, n) -> OR `bit` into the (host-mapped) fault word; one pass of
-// float4 loads, the flag touched only by a wave that found one
-__global__ void nonfinite_check_kernel(const float4* __restrict__ y4, int64_t n4, const float* __restrict__ tail,
-                                       int ntail, unsigned* flag, unsigned bit) {
+// any non-finite value of y[0, n) -> OR `bit` into the (host-mapped) fault word; one grid-stride
+// pass (float4 loads when y is 16-byte aligned, else element-wise), the flag touched only by a
+// wave that found one
+template <bool VEC>
+__global__ void nonfinite_check_kernel(const float* __restrict__ y, int64_t n, unsigned* flag, unsigned bit) {
     bool bad = false;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const float4 v = y4[i];
-        bad |= !__builtin_isfinite(v.x) || !__builtin_isfinite(v.y) || !__builtin_isfinite(v.z) ||
-               !__builtin_isfinite(v.w);
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if constexpr (VEC) {
+        const float4* y4 = reinterpret_cast<const float4*>(y);
+        const int64_t n4 = n / 4;
+        for (int64_t i = i0; i < n4; i += step) {
+            const float4 v = y4[i];
+            bad |= !__builtin_isfinite(v.x) || !__builtin_isfinite(v.y) || !__builtin_isfinite(v.z) ||
+                   !__builtin_isfinite(v.w);
+        }
+        if (i0 < n - 4 * n4) bad |= !__builtin_isfinite(y[4 * n4 + i0]);
+    } else {
+        for (int64_t i = i0; i < n; i += step) bad |= !__builtin_isfinite(y[i]);
     }
-    if (blockIdx.x == 0 && threadIdx.x < ntail) bad |= !__builtin_isfinite(tail[threadIdx.x]);
     if (__any(bad) && (threadIdx.x & 63) == 0)
         __hip_atomic_fetch_or(flag, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -221,19 +230,13 @@ __global__ void nonfinite_check_kernel(const float4* __restrict__ y4, int64_t n4
 
 hipError_t launch_nonfinite_check(const float* y, int64_t n, unsigned* flag, unsigned bit, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    const int64_t n4 = ((reinterpret_cast<uintptr_t>(y) & 15) == 0) ? n / 4 : 0;
-    const int ntail = (int)(n - 4 * n4);
-    if (ntail > 256) {  // unaligned and long: check element-wise through the tail path in chunks
-        for (int64_t off = 0; off < n; off += 256) {
-            const int cnt = (int)std::min<int64_t>(256, n - off);
-            hipLaunchKernelGGL(nonfinite_check_kernel, dim3(1), dim3(256), 0, s, (const float4*)y, (int64_t)0,
-                               y + off, cnt, flag, bit);
-        }
-        return hipGetLastError();
-    }
-    const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 1024);
-    hipLaunchKernelGGL(nonfinite_check_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s,
-                       (const float4*)y, n4, y + 4 * n4, ntail, flag, bit);
+    const bool vec = (reinterpret_cast<uintptr_t>(y) & 15) == 0;
+    const int64_t per = vec ? (n + 3) / 4 : n;
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((per + 255) / 256, 1024));
+    if (vec)
+        hipLaunchKernelGGL(nonfinite_check_kernel<true>, dim3(blocks), dim3(256), 0, s, y, n, flag, bit);
+    else
+        hipLaunchKernelGGL(nonfinite_check_kernel<false>, dim3(blocks), dim3(256), 0, s, y, n, flag, bit);
     return hipGetLastError();
 }
 }  // namespace vp3d

@@ -385,6 +385,17 @@ int ensure_fault_word(vp3d_handle* h) {
     return VP3D_OK;
 }
 
+// the control block (vp3d::SplitCtl: wait bound, fault word, fault injection) into the split
+// workspace, staged in the handle (the source of the async copy lives as long as the handle)
+int write_split_ctl(vp3d_handle* h, unsigned long long spin, int drop, hipStream_t s) {
+    h->sk_ctl_stage = vp3d::SplitCtl{spin, h->sk_err_dev, drop, 0};
+    HIP_TRY(hipMemcpyAsync((char*)h->sk_ws + kSplitPartBytes + vp3d::kSplitCtlOffset, &h->sk_ctl_stage,
+                           sizeof(vp3d::SplitCtl), hipMemcpyHostToDevice, s));
+    h->sk_ctl_spin = spin;
+    h->sk_ctl_drop = drop;
+    return VP3D_OK;
+}
+
 int ensure_split_ws(vp3d_handle* h, hipStream_t s) {
     if (h->sk_ws) return VP3D_OK;
     if (const int rc = ensure_fault_word(h)) return rc;
@@ -396,11 +407,12 @@ int ensure_split_ws(vp3d_handle* h, hipStream_t s) {
         return fail(VP3D_ERR_HIP, std::string("split-K flags: ") + hipGetErrorString(e));
     }
     h->sk_ws = ws;
-    return VP3D_OK;
+    // the production control block, written once with the workspace (no synchronisation)
+    return write_split_ctl(h, vp3d::kSplitSpinTicks, 0, s);
 }
 
 // the workspace into p when a4 would split this layer (allocated then), else none; the
-// control block (vp3d::SplitCtl) follows VP3D_A4_SPLIT_SPIN_TICKS / VP3D_A4_SPLIT_DROP (tests)
+// control block follows VP3D_A4_SPLIT_SPIN_TICKS / VP3D_A4_SPLIT_DROP (fault-injection tests)
 int attach_split_ws(vp3d_handle* h, ConvGemmParams& p, hipStream_t s) {
     if (!conv_gemm_a4_would_split(p)) return VP3D_OK;
     const int rc = ensure_split_ws(h, s);
@@ -410,13 +422,9 @@ int attach_split_ws(vp3d_handle* h, ConvGemmParams& p, hipStream_t s) {
     const unsigned long long spin = sp ? strtoull(sp, nullptr, 10) : vp3d::kSplitSpinTicks;
     const int drop = dr && atoi(dr) != 0 ? 1 : 0;
     if (spin != h->sk_ctl_spin || drop != h->sk_ctl_drop) {
-        static vp3d::SplitCtl ctl;  // the source of an async copy: outlives the call
-        ctl = vp3d::SplitCtl{spin, h->sk_err_dev, drop, 0};
-        HIP_TRY(hipMemcpyAsync((char*)h->sk_ws + kSplitPartBytes + vp3d::kSplitCtlOffset, &ctl, sizeof(ctl),
-                               hipMemcpyHostToDevice, s));
+        // tests only: the staging copy may still be the source of the previous async copy
         HIP_TRY(hipStreamSynchronize(s));
-        h->sk_ctl_spin = spin;
-        h->sk_ctl_drop = drop;
+        if (const int rc2 = write_split_ctl(h, spin, drop, s)) return rc2;
     }
     p.sk_part = (float*)h->sk_ws;
     p.sk_flag = (int*)((char*)h->sk_ws + kSplitPartBytes);
@@ -561,10 +569,15 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         return fail(VP3D_ERR_ARG, "input of " + std::to_string(T) +
                                       " frames does not fit the receptive field of " +
                                       std::to_string(vp3d_receptive_field(h)));
-    // a split-K timeout of an earlier launch on this handle (no synchronisation: the word is
-    // host-mapped); sticky until vp3d_sync_status
-    if (h->sk_err_host && *(volatile unsigned*)h->sk_err_host)
-        return fail(VP3D_ERR_STATE, fault_msg(*(volatile unsigned*)h->sk_err_host));
+    // a fault of an earlier launch on this handle (no synchronisation: the word is host-mapped),
+    // pending until vp3d_sync_status reports and clears it.  A split-K timeout refuses every
+    // forward (the tile flags need re-zeroing); an f16x3 range / non-finite fault refuses only
+    // f16x3 forwards, so the fp32 re-run its message recommends goes through
+    if (h->sk_err_host) {
+        const unsigned fw = *(volatile unsigned*)h->sk_err_host;
+        if ((fw & vp3d::kFaultSplitTimeout) || (fw && dtype == VP3D_DTYPE_F16X3))
+            return fail(VP3D_ERR_STATE, fault_msg(fw));
+    }
     int rc = ensure_ws(h, B, T, dtype);
     if (rc) return rc;
 
@@ -1454,6 +1467,15 @@ int vp3d_stream_serve_begin(vp3d_stream* st, void* stream, double idle_ms) {
     }
     // the stream position of the device (any earlier launches on `stream` finished)
     HIP_TRY(hipStreamSynchronize(s));
+    if (st->fold) {
+        // the host-side shrink affine of the folded form, from the handle's CURRENT weights:
+        // vp3d_load_weights rewrites them in place after the stream was created, and the
+        // resident launch below loads the other layers' weights now too
+        const Layer& sl = h->layers.back();
+        const int nout = sl.cout;
+        HIP_TRY(hipMemcpy(st->shrink_scale.data(), sl.scale, 4 * nout, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(st->shrink_shift.data(), sl.shift, 4 * nout, hipMemcpyDeviceToHost));
+    }
     int pos = 0;
     HIP_TRY(hipMemcpy(&pos, st->frames_seen, 4, hipMemcpyDeviceToHost));
     st->host_t = pos;
@@ -1541,8 +1563,10 @@ int vp3d_stream_serve_wait(vp3d_stream* st, int64_t frame_index, float* pose, do
     };
     if (pose) {
         if (st->fold) {
-            // the shrink role's sum (stream_pipe.hip): partials in workgroup order, then the
-            // affine -- the same f32 operations, so the same bits as the graph form
+            // the shrink folded into the last 1x1 group: its per-workgroup partial sums added
+            // here in workgroup order, then the affine.  The graph form's shrink sums the same
+            // products in another order, so served poses match it within 1e-6 m, not bit for
+            // bit (deterministic from run to run)
             for (int i = 0; i < nout; ++i) {
                 float a = val(i);
                 for (int w = 1; w < st->n_parts; ++w) a += val((size_t)w * 64 + i);

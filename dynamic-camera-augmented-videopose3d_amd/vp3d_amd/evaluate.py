@@ -93,6 +93,12 @@ def evaluate(generator, model: Callable, metrics, action: str | None = None, ver
             infos.append(info)
             # mean per-joint GT displacement per frame (run.py:727-730)
             motion.append(float(torch.linalg.norm(torch.diff(batch_3d.double(), dim=1), dim=-1).mean()))
+    # every forward but the last was checked for device-side faults by the next one (the handle
+    # refuses a call while a fault is pending); the last one is checked here, before any of
+    # these errors is reported (split-K timeout, f16x3 range: RuntimeError)
+    sync = getattr(model, "sync_status", None)
+    if callable(sync):
+        sync()
     res = tuple(float((v / N) * 1000) for v in (e1, e2, e3, ev))  # run.py:762-765 order
     if verbose:
         print("----" + action + "----" if action else "----------")

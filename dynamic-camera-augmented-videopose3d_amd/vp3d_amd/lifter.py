@@ -139,8 +139,15 @@ class NativeLifter:
         return out
 
     def sync_status(self) -> None:
-        """Synchronise the current stream; raise RuntimeError if a launch of this lifter
-        reported a device-side fault (vp3d_sync_status: a split-K owner that timed out)."""
+        """Synchronise the current stream; raise RuntimeError once if a launch of this lifter
+        reported a device-side fault, and clear it (vp3d_sync_status).  The fault kinds:
+          * split-K timeout -- an owner tile of a split partial round stopped waiting for its
+            helper units (its outputs are wrong); refuses EVERY forward until cleared here;
+          * f16x3 range / non-finite -- an activation split into f16 halves was past |x| <=
+            65,504, or the poses came out non-finite; refuses f16x3 forwards only (run those
+            inputs in fp32).
+        A forward raises a pending fault of an earlier forward at entry; the last forward of
+        a run is only checked by calling this (vp3d_amd.evaluate does, after its loop)."""
         with torch.cuda.device(self.device):
             N.check(self._lib.vp3d_sync_status(self._h, N.stream_ptr(self.device)), "vp3d_sync_status")
 

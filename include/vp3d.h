@@ -123,7 +123,8 @@ int vp3d_forward(vp3d_handle* h, const float* x, int B, int T, float* y, int dty
  * wrong -- or when an f16x3 forward split a value past the f16 range of its halves
  * (|x| > 65,504: checked where the input rows and every hidden activation are split) or
  * produced non-finite poses (run such inputs in fp32); the fault is cleared by this call.  (The next vp3d_forward* on the handle also
- * refuses with VP3D_ERR_STATE while the fault is pending, without synchronising.)  No
+ * refuses with VP3D_ERR_STATE while the fault is pending, without synchronising -- every
+ * dtype after a split-K timeout, f16x3 only after an f16x3 range fault.)  No
  * reference counterpart: torch raises asynchronous device errors at the next sync. */
 int vp3d_sync_status(vp3d_handle* h, void* stream);
 
@@ -212,7 +213,8 @@ int vp3d_stream_status(vp3d_stream* s);
  * The last block's 1x1 workgroups fold the shrink in (VP3D_STREAM_FOLD, default on): each
  * stores its channels' partial pose sums and the host adds them in a fixed order (one layer
  * group fewer on the frame's path: median 24.4 vs 25.4 us), so served poses equal the batch
- * form's within 1e-6 m, not bit for bit.  hipFree / hipDeviceSynchronize anywhere in the
+ * form's within 1e-6 m, not bit for bit; the host-side shrink affine is re-read from the
+ * handle at every serve_begin (after vp3d_load_weights too).  hipFree / hipDeviceSynchronize anywhere in the
  * process wait for the resident launch (it ends at idle_ms): end serving before freeing
  * device memory or destroying another stream.
  */

@@ -91,3 +91,64 @@ def test_bench_cli_parses():
     assert out.returncode == 0, out.stderr
     for flag in ("--gpus", "--steps", "--warmup", "--global-batch", "--traj", "--stream"):
         assert flag in out.stdout, flag
+
+
+def _bench(args, env_extra, timeout=300):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=REPO)
+
+
+def test_bench_gpus_n_launches_n_ranks_dry():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (torch.distributed.run child,
+    gloo in the dry mode): ONE line from rank 0 labelled n_gpus 2, the two shards covering the
+    global batch."""
+    r = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1"], {"VP3D_BENCH_DRY": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"] is True and d["steps"] == 3
+    assert d["config"]["windows_per_gpu"] == 32768 and d["config"]["windows_all_ranks"] == 65536
+
+
+def test_bench_world_size_mismatch_refused():
+    """A launcher's WORLD_SIZE that differs from --gpus is refused (rc 2), never mislabelled."""
+    r = _bench(["--gpus", "2"], {"WORLD_SIZE": "4", "VP3D_BENCH_DRY": "1"}, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=4" in r.stderr
+
+
+def test_bench_gpus_n_refused_without_n_devices():
+    """--gpus N > visible GPUs (none in this container) outside a rehearsal: rc 2, no ranks."""
+    r = _bench(["--gpus", "8"], {}, timeout=120)
+    assert r.returncode == 2 and "needs 8 visible GPUs" in r.stderr
+
+
+def test_emit_line_puts_headline_keys_last(capsys):
+    """The driver keeps only the tail of stdout: roofline, cpu_baseline, faults and parity of the
+    headline come after the long legs."""
+    sys.path.insert(0, REPO)
+    import bench
+    bench.emit_line({"metric": "m", "parity": {"a": 1}, "value": 1, "roofline": {}, "config5": {"x": 1},
+                     "cpu_baseline": {}, "faults": 0})
+    keys = list(json.loads(capsys.readouterr().out).keys())
+    assert keys == ["metric", "value", "config5", "roofline", "cpu_baseline", "faults", "parity"]
+
+
+def test_cpu_baseline_child_pins_threads():
+    """The CPU baseline runs the oracle in a child process with one torch thread pinned per
+    distinct physical core (oracle/cpu_timer.py), here on a tiny lifter."""
+    sys.path.insert(0, REPO)
+    import numpy as np
+    import bench
+    from vp3d_amd import synth
+    from common.models.TemporalModel import TemporalModelOptimized1f
+    m = TemporalModelOptimized1f(17, 2, 17, [3, 3], channels=32)
+    sd = synth.lifter_state_dict([(k, tuple(v.shape)) for k, v in m.state_dict().items()], seed=0)
+    x = np.random.default_rng(0).standard_normal((4, 9, 17, 2)).astype(np.float32)
+    c = bench.cpu_baseline(bench.cpu_job("lifter", sd, {"x": x}, fw=[3, 3], strided=True), 4, "poses/s",
+                           "test", repeats=2, target_s=0.05)
+    assert c["value"] > 0 and c["cores"] == len(c["pinned_cpus"]) >= 1 and len(c["runs"]) == 2
+    assert c["threads_pinned"] >= 1 and set(c["pinned_threads_ran_on"]) <= set(c["pinned_cpus"])

@@ -297,3 +297,28 @@ def test_stream_serve_fold_matches_unfolded(monkeypatch):
     d = float(np.abs(out["1"] - out["0"]).max())
     print(f"serve fold vs all-gather shrink: max|d|={d:.3e} m")
     assert d <= 1e-6
+
+
+def test_stream_serve_after_weight_reload_uses_new_shrink():
+    """the folded serve form applies the shrink's affine on the host.  After the
+    stream was created, a parameter change re-uploads the handle's weights in place
+    (TemporalModel.native_lifter -> vp3d_load_weights); serving must then use the NEW shrink
+    bias like the batch form does (serve_begin re-reads it), not the one seen at creation."""
+    fw = (3, 3, 3, 3, 3)
+    m, sd = make_model(False, fw, causal=True)
+    T = 24
+    x = synth.normalized_windows(31, "stream_reload", 1, T)
+    m.cuda()
+    st = CausalStream(m.native_lifter(), "fp32")
+    with torch.no_grad():
+        m.shrink.bias.add_(0.05)
+    assert m.native_lifter() is st.lifter  # the same handle, weights re-uploaded in place
+    with st.serve(idle_ms=500.0) as sv:
+        served = np.stack([sv.step(x[0, t]) for t in range(T)])
+    st.check()
+    st.reset()
+    xs = torch.from_numpy(x[0]).cuda()
+    batch = torch.stack([st.step(xs[t]).clone() for t in range(T)]).cpu().numpy()
+    np.testing.assert_allclose(served, batch, rtol=0, atol=1e-6)
+    ref = _ref({k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}, x, fw)
+    assert np.abs(batch - ref).max() <= 2e-5
