@@ -473,6 +473,20 @@ def seq_main(args, world, rank, dev):
         return
     flop = seq_flop_per_pose(kind)
     poses_s = world * N * args.steps / dt
+    # parity: the first P poses (a time shard: frames [0, P + W - 1)) vs the oracle's sliding
+    # window (oracle/seq_lifter_ref.py: CamTransformer.py:86-89 unfold + the eval forward)
+    from oracle.seq_lifter_ref import lstm_forward, sliding_windows, transformer_forward
+    P = min(64, N)
+    w2, wc = sliding_windows(x2[:, :P + W - 1].cpu(), xc[:, :P + W - 1].cpu(), W)
+    with torch.no_grad():
+        ref = (transformer_forward(sd, w2, wc, 4, 2, 3) if kind == "transformer"
+               else lstm_forward(sd, w2, wc, 128, 2, 3)).reshape(P, JOINTS, 3).numpy()
+    got = y[0, :P].cpu().numpy()
+    gt = synth.gt_poses(3, "seq_lifter_gt", P, JOINTS).reshape(ref.shape)
+
+    def mp(a):
+        return float(np.mean(np.linalg.norm(a.astype(np.float64) - gt, axis=-1)))
+    achieved = poses_s / world * flop / 1e12
     out = {
         "metric": f"3D poses/sec, {'CoupledTransformer' if kind == 'transformer' else 'CoupledLSTM'} sliding window "
                   "(243-frame window, 17 joints, camera-trajectory input)",
@@ -482,9 +496,23 @@ def seq_main(args, world, rank, dev):
         "config": {"workload": f"sliding_window of {kind} over {L} frames (run.py:713)", "poses_per_step": N,
                    "parallelism": f"dp{world} (independent sequences)"},
         "flop_per_pose": flop, "tflops_effective": round(poses_s * flop / 1e12, 3),
+        # every Linear (projections, attention in/out, feed-forward, LSTM gates, head) runs on the
+        # f32 MFMA GEMM or the MFMA attention / LSTM kernels: the step is priced as a whole
+        # against the f32 MFMA peak (per GPU), like --train
+        "roofline": {"bound": "mfma", "kernel": "whole sliding_window step (all launches)",
+                     "achieved": round(achieved, 3), "peak": 157.3, "unit": "TFLOP/s",
+                     "frac": round(achieved / 157.3, 4), "traffic": None,
+                     "note": "algorithmic FLOP per pose (seq_flop_per_pose: 2 x MACs of every Linear, QK^T and "
+                             "PV, the input projection once per frame; softmax / LayerNorm / activations "
+                             "excluded) x poses/s per GPU"},
+        "faults": 0,
+        "parity": {"poses_checked": P, "f32_max_coord_delta_mm": float(np.abs(got - ref).max()) * 1e3,
+                   "f32_mpjpe_delta_mm": abs(mp(got) - mp(ref)) * 1e3,
+                   "meets_north_star_1e-4mm": bool(abs(mp(got) - mp(ref)) * 1e3 <= 1e-4),
+                   "reference": "oracle/seq_lifter_ref.py sliding windows (CamTransformer.py:72-205 / "
+                                "CamLSTM.py:33-129, eval mode) on the same frames and weights"},
     }
     if args.cpu_seconds > 0:
-        from oracle.seq_lifter_ref import sliding_windows
         w2, wc = sliding_windows(x2[:, :64 + W - 1].cpu(), xc[:, :64 + W - 1].cpu(), W)
         fn = cpu_job(kind, sd, {"x": w2, "xc": wc})
         out["cpu_baseline"] = cpu_baseline(fn, 64, "poses/s", "64 sliding windows per run through "
