@@ -731,15 +731,18 @@ def cpu_baseline(job, units_per_run, unit, sample_desc, repeats=5, target_s=2.5,
            "affinity_cpus": affinity, "affinity_physical_cores": n_phys, "cgroup_cpu_quota": cgroup_cpu_quota(),
            **info,
            "threads_note": "torch threads = physical cores capped by the job's CPU share (OMP_NUM_THREADS), one "
-                           "thread pinned per distinct physical core (first logical CPU of each core in "
-                           "sched_getaffinity; OMP_PLACES + OMP_PROC_BIND=close in a child process)"}
+                           "thread pinned per distinct physical core (the least-busy cores of sched_getaffinity "
+                           "by a 0.3 s /proc/stat sample, the idler sibling of each; OMP_PLACES + "
+                           "OMP_PROC_BIND=close in a child process)"}
     if all_cores and n_phys > len(cpus):
         allc, _ = pick_cores(None)
         r2 = _timer_child(job, units_per_run, allc, max(0.6, target_s / 3), 3)
         out["all_physical_cores"] = {"value": r2["value"], "cores": len(allc), "runs": r2["runs"],
                                      "spread": r2["spread"],
                                      "note": "side figure: one thread per physical core of the whole affinity "
-                                             "set, beyond the job's CPU share (other jobs may share these cores)"}
+                                             "set, beyond the job's CPU share: under a cgroup quota "
+                                             "(cgroup_cpu_quota CPUs) these threads share that quota, and other "
+                                             "jobs may share these cores"}
     return out
 
 

@@ -6,8 +6,8 @@ bench.py writes one job file (inputs, the model's state dict, what to run) and s
 
 as a CHILD process (the bench process keeps the GPU; this one never touches it) whose
 environment pins the torch-CPU threads one per physical core: the parent picks the CPUs
-(`pick_cores`: the first logical CPU of distinct physical cores inside the parent's
-sched_getaffinity set), sets OMP_NUM_THREADS / OMP_PLACES={c0},{c1},... / OMP_PROC_BIND=close,
+(`pick_cores`: one logical CPU of each of the least-busy physical cores inside the parent's
+sched_getaffinity set, from a /proc/stat sample), sets OMP_NUM_THREADS / OMP_PLACES={c0},{c1},... / OMP_PROC_BIND=close,
 and this module narrows its own affinity to those CPUs before torch loads.  It then times the
 oracle (the reference's torch-CPU op sequence, oracle/temporal_ref.py etc.) exactly like the
 in-process baseline did -- one warm-up, a calibration run, `repeats` timed runs of ~target_s --
@@ -44,16 +44,49 @@ def physical_cores(cpus):
     return groups
 
 
+def cpu_busy(cpus, window_s=0.3):
+    """{logical cpu: busy fraction over `window_s`} from two /proc/stat samples (empty when
+    /proc/stat is unreadable)."""
+    def sample():
+        out = {}
+        try:
+            with open("/proc/stat") as f:
+                for ln in f:
+                    if ln.startswith("cpu") and ln[3:4].isdigit():
+                        parts = ln.split()
+                        v = [int(x) for x in parts[1:]]
+                        idle = v[3] + (v[4] if len(v) > 4 else 0)  # idle + iowait
+                        out[int(parts[0][3:])] = (sum(v[:8]), idle)
+        except (OSError, ValueError):
+            pass
+        return out
+    a = sample()
+    time.sleep(window_s)
+    b = sample()
+    busy = {}
+    for c in cpus:
+        if c in a and c in b:
+            dt = b[c][0] - a[c][0]
+            busy[c] = 1.0 - (b[c][1] - a[c][1]) / dt if dt > 0 else 0.0
+    return busy
+
+
 def pick_cores(n=None):
-    """The first logical CPU of each distinct physical core in this process's affinity set,
-    the first `n` of them (all when n is None), plus the count of physical cores available."""
+    """One logical CPU of each of the `n` least-busy physical cores in this process's affinity
+    set (all cores when n is None), plus the count of physical cores available.  The boxes are
+    shared by the other GPUs' jobs: a fixed choice (the first n cores) landed on cores other
+    processes kept busy (round 6: 2,908 -> 271 poses/s over five runs), so the choice follows a
+    0.3 s /proc/stat sample -- a core's busy fraction is that of its busier sibling, and the
+    idler sibling is the one pinned."""
     try:
         allowed = os.sched_getaffinity(0)
     except (AttributeError, OSError):
         allowed = set(range(os.cpu_count() or 1))
     groups = physical_cores(allowed)
-    firsts = [v[0] for _, v in sorted(groups.items(), key=lambda kv: kv[1][0])]
-    return (firsts if n is None else firsts[:n]), len(firsts)
+    busy = cpu_busy(allowed) if n is not None else {}
+    ranked = sorted(groups.values(), key=lambda v: (max(busy.get(c, 0.0) for c in v), v[0]))
+    picks = [min(v, key=lambda c: (busy.get(c, 0.0), c)) for v in ranked]
+    return (picks if n is None else sorted(picks[:n])), len(picks)
 
 
 def cgroup_cpu_quota():
