@@ -1206,6 +1206,7 @@ bool conv_gemm_a4_eligible(const ConvGemmParams& p, Act a_type, Act out_type, Ac
 }
 
 static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3, int* level = nullptr);
+static bool a4_tail_split(const ConvGemmParams& p, int mt_tail, int level, bool need_ws);
 
 bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32) {
     if (p.Ktap % GK != 0 || p.Kp % GK != 0 || p.lda % 8 != 0) return false;
@@ -1296,9 +1297,30 @@ static int a4_hn_tail(const ConvGemmParams& p, int ntiles, bool x3, int* level) 
     return L / ntn;
 }
 
+// Split-K tail (conv_gemm_tail.hip, round 6): an f16x3 tail of <= a quarter round (the quarter-N
+// level) after at least one whole round -- sequence mode's 4-tile tails -- runs as (N / 64) x S
+// slices of its K range over every CU plus a reduction launch, instead of 4L quarter-N tiles each
+// a full-K chain on one CU.  Not the whole tiles' bits (S partial chains), so the half-N tails
+// of config 4's shards (8 x 8,192 windows == one 65,536 forward, bit for bit) keep their tiles.
+// The 16-bit layers (bf16 / fp16), which run such tails as a fifth round of whole tiles, take the
+// same split tail (launch_conv_gemm_tail16).  VP3D_A4_TAIL=hn (measurement, read at every launch)
+// keeps the quarter-N tiles / whole tiles; VP3D_A4_SPLIT=0 as well.
+static bool a4_tail_split(const ConvGemmParams& p, int mt_tail, int level, bool need_ws) {
+    if (level != 2 || mt_tail <= 0) return false;
+    const char* e = getenv("VP3D_A4_TAIL");
+    if (e && strcmp(e, "hn") == 0) return false;
+    const char* sp = getenv("VP3D_A4_SPLIT");  // 0: whole tiles only (no split-K of any kind)
+    if (sp && atoi(sp) == 0) return false;
+    const int mt0 = (p.M + GM - 1) / GM - mt_tail;
+    if (mt0 <= 0) return false;  // no whole round: the quarter-N tiles (bit-identical across batch sizes)
+    return conv_gemm_tail_fits(p, mt0 * GM, a4_cus(), need_ws);
+}
+
 bool conv_gemm_a4_would_split(const ConvGemmParams& p) {
     const int ntiles = ((p.M + GM - 1) / GM) * (p.N / GN);
-    if (a4_hn_tail(p, ntiles, true) > 0) return false;  // (the split workspace: f16x3 layers)
+    int level = 1;
+    const int hn = a4_hn_tail(p, ntiles, true, &level);
+    if (hn > 0) return a4_tail_split(p, hn, level, false);  // (the split workspace: f16x3 layers)
     ConvGemmParams q = p;
     a4_split_plan(q, ntiles, p.Kp / GK, false);
     return q.sk_split > 1;
@@ -1324,9 +1346,7 @@ static void a4_launch(const ConvGemmParams& p, dim3 grid, bool split, hipStream_
 // the whole rounds (M-tiles below ntm - mt_tail, if any; walked by one workgroup per CU when
 // `walk_cus` > 0) then the tail as half-N units
 template <typename CT, int X3>
-static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t stream, int walk_cus = 0, int level = 1) {
-    const int ntm = (p.M + GM - 1) / GM;
-    const int mt0 = ntm - mt_tail;
+static void a4_launch_whole(const ConvGemmParams& p, int mt0, hipStream_t stream, int walk_cus) {
     if (mt0 > 0) {
         ConvGemmParams q = p;
         q.M = mt0 * GM;
@@ -1335,6 +1355,13 @@ static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t strea
         const dim3 g(walk_cus > 0 && tiles > walk_cus ? walk_cus : tiles);
         hipLaunchKernelGGL((conv_gemm_a4<CT, 0, X3, true, false>), g, dim3(256), 0, stream, q);
     }
+}
+
+template <typename CT, int X3>
+static void a4_launch_hn(const ConvGemmParams& p, int mt_tail, hipStream_t stream, int walk_cus = 0, int level = 1) {
+    const int ntm = (p.M + GM - 1) / GM;
+    const int mt0 = ntm - mt_tail;
+    a4_launch_whole<CT, X3>(p, mt0, stream, walk_cus);
     ConvGemmParams t = p;
     t.sk_split = t.sk_left = 0;
     t.sk_full = mt0;  // the HN launch's first M-tile
@@ -1371,6 +1398,16 @@ hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p_in, bool out_f32, hipS
     if (hn_tail > 0) {
         // the whole rounds walked as without the tail (the 1x1 + residual layers)
         const int wc = walk_mode > 0 && p.R != nullptr ? a4_cus() : 0;
+        if (a4_tail_split(p, hn_tail, hn_level, true)) {
+            // a tail of <= a quarter round after whole rounds (sequence mode): split over every
+            // CU in its K range too (conv_gemm_tail.hip), not as 4L quarter-N full-K chains
+            const int mt0 = (p.M + GM - 1) / GM - hn_tail;
+            if (out_f32)
+                a4_launch_whole<_Float16, 2>(p, mt0, stream, wc);
+            else
+                a4_launch_whole<_Float16, 1>(p, mt0, stream, wc);
+            return launch_conv_gemm_tail_x3(p, mt0 * GM, out_f32, a4_cus(), stream);
+        }
         if (out_f32)
             a4_launch_hn<_Float16, 2>(p, hn_tail, stream, wc, hn_level);
         else
@@ -1435,6 +1472,25 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p_in, Act compute, hipStrea
         return hipGetLastError();
     }
 #endif
+    {
+        // a tail of <= a quarter round after whole rounds (sequence mode: 4 tiles past 4 rounds):
+        // the whole rounds as the layer would run them, the tail split over every CU
+        int lvl = 1;
+        const int mt_tail = walk_mode == 2 ? 0 : a4_hn_tail(p, ntiles, true, &lvl);  // (the f16x3 tail shape)
+        if (mt_tail > 0 && a4_tail_split(p, mt_tail, lvl, true)) {
+            const int mt0 = (p.M + GM - 1) / GM - mt_tail;
+            const int tiles = mt0 * (p.N / GN);
+            const bool wk = walk_mode > 0 && p.R != nullptr && ncu > 0 && nk >= 3 && tiles > ncu && nk % 2 == 0;
+            ConvGemmParams q = p;
+            q.M = mt0 * GM;
+            q.sk_split = q.sk_full = q.sk_left = 0;
+            if (compute == Act::BF16)
+                a4_launch<__bf16, 0>(q, dim3(wk ? ncu : tiles), false, stream);
+            else
+                a4_launch<_Float16, 0>(q, dim3(wk ? ncu : tiles), false, stream);
+            return launch_conv_gemm_tail16(p, mt0 * GM, compute, ncu, stream);
+        }
+    }
     a4_split_plan(p, ntiles, nk);
     const bool split = p.sk_split > 1;
     const int nunits = split ? p.sk_full + p.sk_split * p.sk_left : ntiles;

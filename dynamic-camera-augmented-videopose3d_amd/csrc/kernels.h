@@ -97,6 +97,15 @@ hipError_t launch_conv_gemm_a4(const ConvGemmParams& p, Act compute, hipStream_t
 // bits as conv_gemm_q64_x3.
 bool conv_gemm_a4_x3_eligible(const ConvGemmParams& p, bool out_f32);
 hipError_t launch_conv_gemm_a4_x3(const ConvGemmParams& p, bool out_f32, hipStream_t stream);
+// Split-K tail of an a4 launch (conv_gemm_tail.hip): rows [m_begin, M) as (N / 64) x S
+// K-slices of 256 x 64 over `ncu` CUs, f32 partials in p.sk_part (the split workspace), then
+// one reduction launch with a4's epilogue -- the split-fp16 one (x3) or the 16-bit one (bf16 /
+// fp16 rows, BN + ReLU [+ residual]).  fits: the shape and (need_ws) the workspace.
+bool conv_gemm_tail_fits(const ConvGemmParams& p, int m_begin, int ncu, bool need_ws);
+hipError_t launch_conv_gemm_tail_x3(const ConvGemmParams& p, int m_begin, bool out_f32, int ncu,
+                                    hipStream_t stream);
+hipError_t launch_conv_gemm_tail16(const ConvGemmParams& p, int m_begin, Act compute, int ncu,
+                                   hipStream_t stream);
 // Split-fp16 mode of conv_gemm_q64 (VP3D_DTYPE_F16X3): A / W / residual rows of f16 halves,
 // each 32-wide K group [hi(32) | lo(32)] (Ktap, Kp, lda, ldr in halves); output split
 // (ldy halves) or, out_f32, f32 rows (ldy floats).  N % 64 == 0, N <= 1024.

@@ -20,7 +20,7 @@ INCLUDE = os.path.join(REPO, "include")
 BUILD_DIR = os.path.join(ROOT_PKG, "build")
 LIB_PATH = os.path.join(PKG_DIR, "libvp3d.so")
 
-SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_8p.hip", "conv_gemm_q64.hip", "conv_gemm_a4.hip", "expand_gemm.hip", "preprocess.hip",
+SOURCES = ["conv_gemm.hip", "conv_gemm_big.hip", "conv_gemm_8p.hip", "conv_gemm_q64.hip", "conv_gemm_a4.hip", "conv_gemm_tail.hip", "expand_gemm.hip", "preprocess.hip",
            "metrics.hip", "stream_step.hip", "stream_persist.hip", "stream_pipe.hip", "train.hip", "seq_lifter.hip", "vp3d_capi.cpp", "vp3d_train.cpp",
            "vp3d_seq.cpp"]
 ARCH = os.environ.get("VP3D_OFFLOAD_ARCH", "gfx950")

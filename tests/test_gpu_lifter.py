@@ -212,12 +212,14 @@ def test_dilated_seq_a4_bit_identical_to_q64(dtype, monkeypatch):
 
 def test_dilated_seq_quarter_n_tail_bit_identical(monkeypatch):
     """Sequence mode at the bench's length (65,778 frames in, 65,536 poses): every block layer
-    is 4 rounds + 4 tiles, which f16x3 runs as 16 quarter-N tiles of 256 x 64 (k3 and 1x1 +
-    residual, dilated taps) -- the same bits as q64."""
+    is 4 rounds + 4 tiles, which f16x3 runs (VP3D_A4_TAIL=hn) as 16 quarter-N tiles of 256 x 64
+    (k3 and 1x1 + residual, dilated taps) -- the same bits as q64.  The default since round 6
+    splits that tail's K range over every CU (test_dilated_seq_split_tail)."""
     model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
     x = synth.normalized_windows(1, "x1_65778", 1, 65778)
     model.cuda().set_compute_dtype("f16x3")
     xd = torch.from_numpy(x).cuda()
+    monkeypatch.setenv("VP3D_A4_TAIL", "hn")
     ys = {}
     for gemm in ("q64", "a4"):
         monkeypatch.setenv("VP3D_GEMM", gemm)
@@ -225,6 +227,53 @@ def test_dilated_seq_quarter_n_tail_bit_identical(monkeypatch):
             ys[gemm] = model(xd).cpu().numpy()
     assert np.isfinite(ys["a4"]).all()
     assert np.array_equal(ys["a4"], ys["q64"]), np.abs(ys["a4"] - ys["q64"]).max()
+
+
+@pytest.mark.parametrize("dtype", ["f16x3", "bf16"])
+def test_dilated_seq_split_tail(dtype, monkeypatch):
+    """The default f16x3 sequence-mode tail (conv_gemm_tail.hip): the 4 tiles past the 4 whole
+    rounds of every block layer as (N / 64) x S K-slices over every CU plus a reduction launch.
+    Against the quarter-N tiles (one full-K chain per output, VP3D_A4_TAIL=hn): every pose
+    within 5e-6 m (S partial chains instead of one: f32 rounding of the partial sums only; the
+    tails are the last 242 frames' outputs of every layer, which reach every pose through the
+    receptive field), deterministic run to run, and against the oracle under the fp32 gates on
+    the first and last output frames (the last ones are computed from the tail rows).  bf16
+    (whole tiles in a fifth round otherwise): deterministic, and the bf16 gates vs the oracle."""
+    model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
+    x = synth.normalized_windows(1, "x1_65778", 1, 65778)
+    model.cuda().set_compute_dtype(dtype)
+    xd = torch.from_numpy(x).cuda()
+    ys = {}
+    for name, tail in (("hn", "hn"), ("split", None), ("split2", None)):
+        if tail:
+            monkeypatch.setenv("VP3D_A4_TAIL", tail)
+        else:
+            monkeypatch.delenv("VP3D_A4_TAIL", raising=False)
+        with torch.no_grad():
+            ys[name] = model(xd).cpu().numpy()
+    model.native_lifter(torch.device("cuda")).sync_status()
+    assert np.isfinite(ys["split"]).all()
+    assert np.array_equal(ys["split"], ys["split2"])  # deterministic
+    assert not np.array_equal(ys["split"], ys["hn"])  # the split path ran
+    if dtype == "f16x3":
+        d = np.abs(ys["split"] - ys["hn"]).max()
+        assert d <= 5e-6, d  # (measured 1.07e-6 m: the same order as f16x3's own max error vs fp32)
+    P = 64
+    for lo in (0, 65536 - P):
+        ref = lifter_forward(sd, x[:, lo:lo + P + 242], (3, 3, 3, 3, 3)).numpy()
+        got = ys["split"][:, lo:lo + P]
+        if dtype == "f16x3":
+            assert np.abs(got - ref).max() <= 1e-5, (lo, np.abs(got - ref).max())
+        else:
+            # bf16: the coordinate gate, and the split tail's MPJPE delta against the whole tiles'
+            # (a 64-frame delta of bf16 is noisy: both are printed)
+            gt = synth.gt_poses(3, "gt", P, 17).reshape(ref.shape)
+            hn = ys["hn"][:, lo:lo + P]
+            d_s = abs(mpjpe_np(got, gt) - mpjpe_np(ref, gt)) * 1e3
+            d_h = abs(mpjpe_np(hn, gt) - mpjpe_np(ref, gt)) * 1e3
+            e_s, e_h = np.abs(got - ref).max(), np.abs(hn - ref).max()
+            print(f"bf16 frames {lo}..: split max|d| {e_s:.3e} m dMPJPE {d_s:.4f} mm; whole tiles {e_h:.3e} m {d_h:.4f} mm")
+            assert e_s <= H16_TOL[dtype][0], e_s
 
 
 def test_dilated_long_seq_bf16():
