@@ -82,8 +82,12 @@ __device__ __forceinline__ void exp_vm() {
 // registers as 16 bytes of hi and 16 of lo (channel n at 64 (n / 32) + n % 32 of the split
 // row, lo 32 further): no LDS staging, so with a 2-chunk weight ring two workgroups share
 // a CU and one's epilogue runs under the other's MFMAs.
+// RING 1 (X3 only; round 6, the gathered NKS <= 4 shape): one weight chunk resident (32 KB + 8 KB
+// of scale / shift) and RB 2 (154 VGPRs): three workgroups per CU instead of two, each staging its
+// next chunk after the barrier that ends the current one and waiting for it (with the previous
+// chunk's stores: vmcnt retires in order) -- the other two workgroups keep the CU busy meanwhile.
 template <typename CT, int NKS, int RB, bool GATHER, bool NT = false, int RING = 3, bool X3 = false>
-__global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
+__global__ __launch_bounds__(256, (X3 && RING == 1) ? 3 : 2) void expand_gemm_h16(ConvGemmParams p, GatherSrc g) {
     constexpr int kRowsW = 16 * RB;
     constexpr int kRows = kRowsW * kExpWaves;
     constexpr int NKW = X3 ? 2 * NKS : NKS;  // weight slabs per chunk
@@ -283,7 +287,16 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
                 gh4[j] = *(const f32x4*)(p.shift + gc + 16 * j);
             }
         }
-        if (ch + RING - 1 < ch_hi) stage_w(ch + RING - 1);
+        if constexpr (RING == 1) {
+            // the single slot: every wave passed the barrier that ended chunk ch - 1
+            if (ch > ch_lo) {
+                stage_w(ch);
+                exp_vm<0>();
+                __builtin_amdgcn_s_barrier();
+            }
+        } else if (ch + RING - 1 < ch_hi) {
+            stage_w(ch + RING - 1);
+        }
         const char* wb = smem + ((ch - ch_lo) % RING) * kChunk;
         f32x4 acc[RB][4];
         if constexpr (X3) {
@@ -414,7 +427,7 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
             }
             gemm::x3_range_flag(vmax, p.scale, p.N);
             asm volatile("" ::: "memory");
-            if (ch + 1 < ch_hi && !(abl & 4)) {
+            if (RING > 1 && ch + 1 < ch_hi && !(abl & 4)) {
                 if (m_wave + kRowsW > p.M || (abl & 2))
                     exp_vm<0>();
                 else if (RING == 3 && ch + 2 < ch_hi)
@@ -495,14 +508,14 @@ __global__ __launch_bounds__(256, 2) void expand_gemm_h16(ConvGemmParams p, Gath
 // resident workgroup slots per launch: two per CU (__launch_bounds__(256, 2)) for every
 // variant -- the camera-concat NKS = 5 one included since its RB 4 / 2-chunk weight ring
 // (72 KB of LDS)
-static int exp_slots() {
-    static const int n = [] {
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+static int exp_slots(int per_cu = 2) {
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return 0;
-        return 2 * ncu;
+        return n;
     }();
-    return n;
+    return per_cu * ncu;
 }
 
 // One workgroup per row block, except in a partial last round: with L < slots row blocks
@@ -517,7 +530,7 @@ template <typename CT, int RB, bool GATHER, bool NT, int RING = 3, bool X3 = fal
 hipError_t launch_rb_nt(const ConvGemmParams& p_in, const GatherSrc& g, int nks, hipStream_t s) {
     ConvGemmParams p = p_in;
     const int nrb = (p.M + 64 * RB - 1) / (64 * RB);
-    const int slots = exp_slots();
+    const int slots = exp_slots((X3 && RING == 1) ? 3 : 2);
     const int left = slots > 0 ? nrb % slots : 0;
     int S = left > 0 ? slots / left : 1;
     S = S > 8 ? 8 : S;
@@ -646,6 +659,14 @@ hipError_t launch_expand_gemm_x3(const ConvGemmParams& p, const GatherSrc* g, hi
         return (full + (left > 0 ? 1.0 / S : 0.0)) * rb;
     };
     const bool rb3 = cost(3) <= cost(2) + 1e-9;
+    // the gathered config-2/4 shape (K = 102, NKS 4): three workgroups per CU (RING 1, RB 2:
+    // 40 KB of LDS, 154 VGPRs) -- config 4 expand 5.18-5.21 vs 5.30-5.31 ms at B = 65,536, 0.698-0.702
+    // vs 0.703-0.705 at 8,192, same box, forwards bit-identical (profiles/r06_x3_expand_ring1_ab.txt);
+    // VP3D_X3_EXPAND_RING=2 (measurement, read at every launch) keeps the two-per-CU form below
+    const char* ring = getenv("VP3D_X3_EXPAND_RING");
+    if (!(ring && ring[0] == '2') && g && nks <= 4)
+        return nt ? launch_rb_nt<f16, 2, true, true, 1, true>(p, *g, nks, stream)
+                  : launch_rb_nt<f16, 2, true, false, 1, true>(p, *g, nks, stream);
     if (g) {
         if (rb3)
             return nt ? launch_rb_nt<f16, 3, true, true, 2, true>(p, *g, nks, stream)

@@ -364,6 +364,31 @@ def test_shape_asserts_and_short_input():
         m(torch.zeros(1, 5, 17, 2, device="cuda"))
 
 
+@pytest.mark.parametrize("B", [8192, 300])
+def test_x3_expand_three_per_cu_bit_identical(B, monkeypatch):
+    """The f16x3 expand of the gathered config-4 shape runs three workgroups per CU (one
+    resident weight chunk, 2 row blocks per wave) since round 6; the two-per-CU form
+    (VP3D_X3_EXPAND_RING=2: 2-chunk ring, 3 row blocks) computes every output the same way, so
+    the forwards are the same bits (B = 300: one partial round split into channel ranges)."""
+    from vp3d_amd.pipeline import SyntheticWindowPool
+    model, sd = make_model(True, (3, 3, 3, 3, 3), False, 1024)
+    model = model.cuda()
+    lifter = model.native_lifter(torch.device("cuda"))
+    pool = SyntheticWindowPool(3, device="cuda", n_seq=8, seq_len=1024)
+    pairs = torch.from_numpy(pool.global_pairs(B)).cuda()
+    ys = {}
+    for name, env in (("ring1", None), ("ring2", "2")):
+        if env:
+            monkeypatch.setenv("VP3D_X3_EXPAND_RING", env)
+        else:
+            monkeypatch.delenv("VP3D_X3_EXPAND_RING", raising=False)
+        with torch.no_grad():
+            ys[name] = lifter.forward_windows(pool.seqs, pairs, 243, 121, dtype="f16x3").cpu().numpy()
+    lifter.sync_status()
+    assert np.isfinite(ys["ring1"]).all()
+    assert np.array_equal(ys["ring1"], ys["ring2"]), np.abs(ys["ring1"] - ys["ring2"]).max()
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
 def test_f32_narrow_shrink_bit_identical(dtype, monkeypatch):
     """The exact-f32 narrow GEMM that runs the shrink (N = 51) keeps conv_gemm_f32's MFMA k
