@@ -235,6 +235,20 @@ __global__ __launch_bounds__(256) void tail_reduce16_kernel(ConvGemmParams p, in
     *(u32x4*)((CT*)p.Y + (int64_t)m * p.ldy + c8) = pack8<CT>(o);
 }
 
+// the shrink's reduce: one thread per (row, real channel n < N_out): the S partials in slice
+// order, then scale / shift (two roundings, no ReLU), f32 into the pose rows
+__global__ __launch_bounds__(256) void shrink_reduce_x3_kernel(ConvGemmParams p, int n_out, int m_begin, int rows,
+                                                               int rows_pad, int S, const float* __restrict__ part) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)rows * n_out) return;
+    const int mloc = (int)(t / n_out);
+    const int n = (int)(t - (int64_t)mloc * n_out);
+    const float* pp = part + (size_t)mloc * TN + n;
+    float v = pp[0];
+    for (int q = 1; q < S; ++q) v += pp[(size_t)q * rows_pad * TN];
+    ((float*)p.Y)[(int64_t)(m_begin + mloc) * p.ldy + n] = __fadd_rn(__fmul_rn(v, p.scale[n]), p.shift[n]);
+}
+
 }  // namespace
 
 // S for a tail of `rows` rows: about one workgroup per CU, S | Kp / 64, the partials within
@@ -314,4 +328,31 @@ hipError_t launch_conv_gemm_tail_x3(const ConvGemmParams& p, int m_begin, bool o
     return hipGetLastError();
 }
 
+}  // namespace vp3d
+
+namespace vp3d {
+// the f16x3 shrink: p.N = the real output channels (<= 64), p.W = the shrink's split weights
+// (zero rows past N), p.scale = its scale_x3 (padded to 64); rows in chunks whose 2 K-slices of
+// 64-column partials fit the split workspace
+hipError_t launch_conv_gemm_x3_shrink(const ConvGemmParams& p_in, hipStream_t stream) {
+    constexpr int S = 2;
+    const int n_out = p_in.N;
+    if (n_out > TN || !p_in.sk_part || p_in.Kp % (KS * S) != 0 || p_in.Ktap % KS != 0 || p_in.lda % 8 != 0)
+        return hipErrorInvalidValue;
+    ConvGemmParams p = p_in;
+    p.N = TN;
+    const int chunk = (int)(kSplitPartBytes / ((size_t)S * TN * sizeof(float)) / TM * TM);
+    for (int m0 = 0; m0 < p_in.M; m0 += chunk) {
+        const int m1 = m0 + chunk < p_in.M ? m0 + chunk : p_in.M;
+        p.M = m1;  // the row bound of this chunk (rows past it clamp and are not stored)
+        const int rows = m1 - m0;
+        const int mt = (rows + TM - 1) / TM;
+        hipLaunchKernelGGL((tail_split_kernel<f16, true>), dim3(1, S, mt), dim3(256), 0, stream, p, m0, mt * TM,
+                           (p.Kp / KS) / S, p.sk_part);
+        const unsigned blocks = (unsigned)(((int64_t)rows * n_out + 255) / 256);
+        hipLaunchKernelGGL(shrink_reduce_x3_kernel, dim3(blocks), dim3(256), 0, stream, p, n_out, m0, rows, mt * TM, S,
+                           (const float*)p.sk_part);
+    }
+    return hipGetLastError();
+}
 }  // namespace vp3d

@@ -75,7 +75,7 @@ struct Layer {
     // kernel's loader feeds them 1.0); null when K + 2 does not fit in Kp
     uint16_t* wfbf = nullptr;
     uint16_t* wfh = nullptr;
-    // split-fp16 path (VP3D_DTYPE_F16X3, every layer but the shrink): the f32 weights
+    // split-fp16 path (VP3D_DTYPE_F16X3, every layer; the shrink's since round 6): the f32 weights
     // scaled by 2^e (max |W 2^e| in [2^14, 2^15)) and carried as hi + lo f16 halves,
     // [Np][2 Kp] with each 32-wide K group stored [hi(32) | lo(32)]; scale_x3 = scale * 2^-e
     uint16_t* wx3 = nullptr;

@@ -106,6 +106,11 @@ hipError_t launch_conv_gemm_tail_x3(const ConvGemmParams& p, int m_begin, bool o
                                     hipStream_t stream);
 hipError_t launch_conv_gemm_tail16(const ConvGemmParams& p, int m_begin, Act compute, int ncu,
                                    hipStream_t stream);
+// The f16x3 shrink (N = cout <= 64 poses channels, f32 rows of ldy out, scale / shift without
+// ReLU) on the same kernels: every row, 64 columns (W rows past N zero), 2 K-slices, then a
+// reduction that writes the N real channels; p.sk_part = the split workspace (rows in chunks
+// that fit it)
+hipError_t launch_conv_gemm_x3_shrink(const ConvGemmParams& p, hipStream_t stream);
 // Split-fp16 mode of conv_gemm_q64 (VP3D_DTYPE_F16X3): A / W / residual rows of f16 halves,
 // each 32-wide K group [hi(32) | lo(32)] (Ktap, Kp, lda, ldr in halves); output split
 // (ldy halves) or, out_f32, f32 rows (ldy floats).  N % 64 == 0, N <= 1024.

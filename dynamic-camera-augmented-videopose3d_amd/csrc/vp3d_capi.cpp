@@ -256,7 +256,7 @@ int upload_weights(vp3d_handle* h, const float* const* w, int n) {
             HIP_TRY(hipMemcpy(L.wfbf, fbf.data(), fbf.size() * 2, hipMemcpyHostToDevice));
             HIP_TRY(hipMemcpy(L.wfh, fh.data(), fh.size() * 2, hipMemcpyHostToDevice));
         }
-        if (!is_shrink) {
+        {
             // split-fp16 copy: W 2^e = hi + lo, both f16 (hi = f16(W 2^e), lo = f16(W 2^e - hi)),
             // the power of two undone exactly by the epilogue scale.
             // Sign-balanced accumulation: odd output channels carry -W and -scale (exact sign
@@ -283,8 +283,10 @@ int upload_weights(vp3d_handle* h, const float* const* w, int n) {
                     px3[q + 32] = f32_to_f16_rne(v - f16_to_f32(hi));
                 }
             // [cout scales | the fault word's device address] (gemm::x3_range_flag; the kernels
-            // run with cout % 64 == 0, so the address is 8-byte aligned at index cout)
-            const int tail = (L.cout + 1) & ~1;
+            // run with cout % 64 == 0, so the address is 8-byte aligned at index cout).  The
+            // shrink (cout = 51): scales padded with zeros to 64 channels (its split GEMM runs
+            // 64 columns, the W rows past cout are zero), no range guard (f32 poses out)
+            const int tail = is_shrink ? (L.cout + 63) / 64 * 64 : (L.cout + 1) & ~1;
             std::vector<float> scx3(tail + 2, 0.f);
             for (int o = 0; o < L.cout; ++o) scx3[o] = std::ldexp(balance && (o & 1) ? -sc[o] : sc[o], -e);
             static_assert(sizeof(unsigned*) == 2 * sizeof(float), "pointer = two floats");
@@ -429,6 +431,13 @@ int attach_split_ws(vp3d_handle* h, ConvGemmParams& p, hipStream_t s) {
     p.sk_part = (float*)h->sk_ws;
     p.sk_flag = (int*)((char*)h->sk_ws + kSplitPartBytes);
     return VP3D_OK;
+}
+
+// the f16x3 forward's shrink on the split-fp16 tail kernels (default since round 6) or, with
+// VP3D_X3_SHRINK=f32 (measurement; read at every forward), the exact f32 GEMM over f32 rows
+bool x3_split_shrink(const vp3d_handle* h) {
+    const char* e = getenv("VP3D_X3_SHRINK");
+    return !(e && strcmp(e, "f32") == 0) && h->layers.back().cout <= 64;  // (one 64-column block)
 }
 
 constexpr const char* kSplitFaultMsg =
@@ -650,7 +659,20 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
         const Act o_type = last ? Act::F32 : act;
         hipError_t e = hipSuccess;
         bool launched = false;
-        if (x3 && last) {
+        if (x3 && last && x3_split_shrink(h)) {
+            // shrink (round 6): split fp16 over the split rows the layer before wrote, on the
+            // split-K tail kernels (conv_gemm_tail.hip) with a fixed 2 K-slices per output -- the
+            // same sums at every batch size -- and f32 poses out
+            if ((rc = ensure_split_ws(h, s))) return rc;
+            p.W = L.wx3;
+            p.Kp = 2 * L.Kp;
+            p.lda = 2 * L.cin;
+            p.Ktap = 2 * L.Ktap;
+            p.scale = L.scale_x3;
+            p.sk_part = (float*)h->sk_ws;
+            e = launch_conv_gemm_x3_shrink(p, s);
+            launched = true;
+        } else if (x3 && last) {
             // shrink: the exact f32 GEMM over the f32 rows the layer before wrote
             p.W = L.w32;
             e = launch_conv_gemm(p, Act::F32, Act::F32, Act::F32, s);
@@ -691,7 +713,7 @@ static int forward_impl(vp3d_handle* h, const float* x, int B, int T, float* y, 
                 p.lda = 2 * L.cin;
                 p.Ktap = 2 * L.Ktap;
             }
-            const bool out_f32 = li == nl - 2;
+            const bool out_f32 = li == nl - 2 && !x3_split_shrink(h);
             p.Kp = 2 * L.Kp;
             p.W = L.wx3;
             p.scale = L.scale_x3;

@@ -389,11 +389,43 @@ def test_x3_expand_three_per_cu_bit_identical(B, monkeypatch):
     assert np.array_equal(ys["ring1"], ys["ring2"]), np.abs(ys["ring1"] - ys["ring2"]).max()
 
 
+def test_x3_split_shrink(monkeypatch):
+    """Since round 6 the f16x3 forward runs its shrink (N = 51) in split fp16 too, over the split
+    rows of the last block (conv_gemm_tail.hip: 64 columns, a fixed 2 K-slices per output, rows
+    in chunks of 131,072 that fit the split workspace).  One 140,242-frame sequence (two row
+    chunks): within 5e-6 m of the exact-f32 shrink (VP3D_X3_SHRINK=f32, f32 rows from the last
+    block) and under the fp32 gates vs the oracle on the first and last frames."""
+    model, sd = make_model(False, (3, 3, 3, 3, 3), False, 1024)
+    x = synth.normalized_windows(1, "x1_140242", 1, 140242)
+    model.cuda().set_compute_dtype("f16x3")
+    xd = torch.from_numpy(x).cuda()
+    ys = {}
+    for name, env in (("split", None), ("f32", "f32")):
+        if env:
+            monkeypatch.setenv("VP3D_X3_SHRINK", env)
+        else:
+            monkeypatch.delenv("VP3D_X3_SHRINK", raising=False)
+        with torch.no_grad():
+            ys[name] = model(xd).cpu().numpy()
+    model.sync_status()
+    assert np.isfinite(ys["split"]).all()
+    d = np.abs(ys["split"] - ys["f32"]).max()
+    assert d <= 5e-6, d  # (measured 2.0e-6 m over 140,000 poses: the f16x3 products' own error)
+    P = 64
+    for lo in (0, 140000 - P):
+        ref = lifter_forward(sd, x[:, lo:lo + P + 242], (3, 3, 3, 3, 3)).numpy()
+        got = ys["split"][:, lo:lo + P]
+        assert np.abs(got - ref).max() <= 1e-5, (lo, np.abs(got - ref).max())
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "f16x3"])
 def test_f32_narrow_shrink_bit_identical(dtype, monkeypatch):
     """The exact-f32 narrow GEMM that runs the shrink (N = 51) keeps conv_gemm_f32's MFMA k
     order: the same bits as the tile kernel (VP3D_F32_NARROW=0), on a ragged batch (the narrow
-    kernel takes M < 32,768 rows)."""
+    kernel takes M < 32,768 rows).  f16x3: with its exact-f32 shrink (VP3D_X3_SHRINK=f32; the
+    default is the split-fp16 shrink, test_x3_split_shrink)."""
+    if dtype == "f16x3":
+        monkeypatch.setenv("VP3D_X3_SHRINK", "f32")
     model, _ = make_model(True, seed=0)
     model = model.cuda()
     model.set_compute_dtype(dtype)
