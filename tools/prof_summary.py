@@ -63,7 +63,8 @@ def main():
 def per_layer(trace, B):
     """Per-layer durations by dispatch order: a forward of batch B starts at its expand
     dispatch (fused expand kernel, grid = ceil(B*81/256)*256 threads) and is followed by
-    the 9 conv-GEMM dispatches of blocks 1-4 and the shrink."""
+    the 9 conv-GEMM dispatches of blocks 1-4 (each with its split-K tail launches, if any) and
+    the shrink (a conv-GEMM, or the f16x3 shrink's split + reduce launches)."""
     layers = ["expand", "block1_k3", "block1_1x1", "block2_k3", "block2_1x1", "block3_k3",
               "block3_1x1", "block4_k3", "block4_1x1", "shrink"]
     rows = []
@@ -81,21 +82,38 @@ def per_layer(trace, B):
     if eg == 0:  # the fp32 path: the expand is the largest conv_gemm_f32 launch
         eg = max((r[2] for r in rows if "conv_gemm_f32" in r[1]), default=0)
         starts = "conv_gemm_f32"
+    # a layer starts at a conv_gemm dispatch, or at a split-K tail dispatch of ONE 64-column
+    # block (the f16x3 shrink since round 6: tail_split_kernel + shrink_reduce_x3_kernel); the
+    # other split-tail and reduce dispatches belong to the layer before them (its tail)
+    def opens(r):
+        return "conv_gemm" in r[1] or ("tail_split_kernel" in r[1] and r[2] == 256)
+
+    def joins(r):
+        return "tail_split_kernel" in r[1] or "reduce" in r[1]
     agg = defaultdict(list)
     names = {}
     i = 0
     while i < len(rows):
         if starts in rows[i][1] and rows[i][2] == eg:
-            seq = [rows[i]]
+            seq = [[rows[i][3], short(rows[i][1])]]
             j = i + 1
-            while j < len(rows) and len(seq) < len(layers):
-                if "conv_gemm" in rows[j][1]:
-                    seq.append(rows[j])
+            while j < len(rows):
+                r = rows[j]
+                if opens(r):
+                    if len(seq) == len(layers):
+                        break
+                    seq.append([r[3], short(r[1]) if "conv_gemm" in r[1] else "tail_split_kernel + shrink_reduce (f16x3 shrink)"])
+                elif joins(r) and len(seq) > 1:
+                    seq[-1][0] += r[3]
+                    if "+ tail" not in seq[-1][1] and "shrink" not in seq[-1][1]:
+                        seq[-1][1] += " + tail"
+                elif starts in r[1] and r[2] == eg:
+                    break
                 j += 1
             if len(seq) == len(layers):
-                for name, r in zip(layers, seq):
-                    agg[name].append(r[3])
-                    names[name] = short(r[1])
+                for name, (d, k) in zip(layers, seq):
+                    agg[name].append(d)
+                    names[name] = k
             i = j
         else:
             i += 1
