@@ -54,15 +54,33 @@ def forwards(rows, B):
         if not start:
             i += 1
             continue
-        seq = [("expand", rows[ids[i]][2])]
+        # a layer starts at a conv_gemm dispatch; split-K tail dispatches (tail_split_kernel,
+        # tail_reduce_*) add to the layer before them, except the f16x3 shrink's (round 6): a
+        # tail_split_kernel followed by shrink_reduce_x3_kernel is the shrink layer itself
+        seq = [["expand", rows[ids[i]][2]]]
+        last_split = 0.0
         j = i + 1
-        while j < len(ids) and len(seq) < len(LAYERS):
+        while j < len(ids):
             n2, g2, v2 = rows[ids[j]]
             if "conv_gemm" in n2:
-                seq.append((LAYERS[len(seq)], v2))
+                if len(seq) == len(LAYERS):
+                    break
+                seq.append([LAYERS[len(seq)], v2])
+                last_split = 0.0
+            elif "tail_split_kernel" in n2 and len(seq) > 1:
+                seq[-1][1] += v2
+                last_split = v2
+            elif "shrink_reduce" in n2 and len(seq) == len(LAYERS) - 1:
+                seq[-1][1] -= last_split
+                seq.append([LAYERS[len(seq)], last_split + v2])
+                last_split = 0.0
+            elif "reduce" in n2 and len(seq) > 1:
+                seq[-1][1] += v2
+            elif "expand_gemm" in n2:
+                break
             j += 1
         if len(seq) == len(LAYERS):
-            yield seq
+            yield [tuple(x) for x in seq]
         i = j
 
 
