@@ -31,7 +31,7 @@ def test_current_default_line():
     """The round's last default line (config 4, f16x3): the accurate path is `value`, priced at
     the f16 peak / 3, with its legs -- bf16 / fp32, config 3, config 5 in fp32 and fp16, the
     sequence mode -- and the north-star gate met by every accurate leg."""
-    d = _line("r05final_bench_default.json")
+    d = _line("r06final_bench_default.json")
     with open(os.path.join(REPO, "BASELINE.json")) as f:
         base = json.load(f)
     assert d["metric"] == base["metric"] and d["dtype"] == "f16x3" and d["n_gpus"] == 1
@@ -50,6 +50,12 @@ def test_current_default_line():
     assert d["config3"]["f16x3"]["mpjpe_delta_mm"] <= 1e-4
     c = d["cpu_baseline"]
     assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["affinity_cpus"] >= 1
+    # round 6: the CPU baseline's threads pinned one per physical core, the line's traffic taken
+    # on the same build, faults checked after every leg, and the headline keys last
+    assert c["threads_pinned"] >= c["cores"] and len(c["runs"]) == 5
+    assert r["traffic"] is not None and r["traffic_source"]["same_build"]
+    assert d["faults"] == 0
+    assert list(d.keys())[-1] == "parity" and "roofline" in list(d.keys())[-7:]
 
 
 @pytest.mark.parametrize("name", HEADLINE)
