@@ -38,45 +38,49 @@ constexpr int KS = 64;   // halves per K-step (one [hi | lo] group of 32 K value
 // 16-byte chunk c of LDS row r sits at c ^ (r & 7), so a fragment read (16 rows, one chunk) is
 // spread over the banks.  (Round 6, first form: fragments straight from global memory, 16
 // rows per load instruction: 44-48 us per k3 tail, 21 us per 1x1 tail.)
-template <typename CT, bool X3>
+// RBW: row blocks of 16 per wave (4: 256 rows per workgroup; 1: 64 rows, the f16x3 shrink of small
+// batches -- 4x the workgroups, the same per-output chains)
+template <typename CT, bool X3, int RBW = 4>
 __global__ __launch_bounds__(256) void tail_split_kernel(ConvGemmParams p, int m_begin, int rows_pad,
                                                          int steps_per_unit, float* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) char smem[2][(TM + TN) * 128];
+    constexpr int TMR = 64 * RBW;  // rows per workgroup
+    constexpr int NA = TMR / 32;   // A rows staged per thread and K-step
+    __shared__ __attribute__((aligned(16))) char smem[2][(TMR + TN) * 128];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wv = tid >> 6;
     const int g = lane >> 4;  // k chunk (8 elements) of this lane in a 32-deep half
     const int n0 = blockIdx.x * TN;
     const int slice = blockIdx.y;
-    const int mt0 = blockIdx.z * TM;  // the workgroup's first row (tail-relative)
+    const int mt0 = blockIdx.z * TMR;  // the workgroup's first row (tail-relative)
     const int s0 = slice * steps_per_unit;
 
-    // staging: this thread's 8 A rows (tid / 8 + 32 i) and 2 W rows (tid / 8 + 32 i), chunk tid % 8
+    // staging: this thread's NA A rows (tid / 8 + 32 i) and 2 W rows (tid / 8 + 32 i), chunk tid % 8
     const int sc = tid & 7;
     const int sr = tid >> 3;
     const CT* const A = (const CT*)p.A;
     const CT* const W = (const CT*)p.W;
-    int srow[8];
+    int srow[NA];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NA; ++i) {
         int m = m_begin + mt0 + sr + 32 * i;
         m = m < p.M ? m : p.M - 1;  // rows past M read a valid row; never stored
         srow[i] = src_row(p, m);
     }
-    u32x4 st[10];
+    u32x4 st[NA + 2];
     auto gload = [&](int s) __attribute__((always_inline)) {
         const int k0 = s * KS;
         const int tap = k0 / p.Ktap;
         const int koff = k0 - tap * p.Ktap + 8 * sc;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) st[i] = *(const u32x4*)(A + (int64_t)(srow[i] + tap * p.dil) * p.lda + koff);
+        for (int i = 0; i < NA; ++i) st[i] = *(const u32x4*)(A + (int64_t)(srow[i] + tap * p.dil) * p.lda + koff);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) st[8 + i] = *(const u32x4*)(W + (size_t)(n0 + sr + 32 * i) * p.Kp + k0 + 8 * sc);
+        for (int i = 0; i < 2; ++i) st[NA + i] = *(const u32x4*)(W + (size_t)(n0 + sr + 32 * i) * p.Kp + k0 + 8 * sc);
     };
     auto lstore = [&](char* buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            const int r = i < 8 ? sr + 32 * i : TM + sr + 32 * (i - 8);
+        for (int i = 0; i < NA + 2; ++i) {
+            const int r = i < NA ? sr + 32 * i : TMR + sr + 32 * (i - NA);
             *(u32x4*)(buf + r * 128 + ((sc ^ (r & 7)) << 4)) = st[i];
         }
     };
@@ -84,9 +88,9 @@ __global__ __launch_bounds__(256) void tail_split_kernel(ConvGemmParams p, int m
     auto frag = [&](const char* buf, int r, int c) __attribute__((always_inline)) -> u32x4 {
         return *(const u32x4*)(buf + r * 128 + ((c ^ (r & 7)) << 4));
     };
-    f32x4 acc[4][4];
+    f32x4 acc[RBW][4];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+    for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
     gload(s0);
@@ -96,21 +100,21 @@ __global__ __launch_bounds__(256) void tail_split_kernel(ConvGemmParams p, int m
     for (int i = 0; i < steps_per_unit; ++i) {
         const char* buf = smem[i & 1];
         if (i + 1 < steps_per_unit) gload(s0 + i + 1);
-        u32x4 fa[4][2], fw[4][2];
+        u32x4 fa[RBW][2], fw[4][2];
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-            fa[rb][0] = frag(buf, 64 * wv + 16 * rb + fr, g);
-            fa[rb][1] = frag(buf, 64 * wv + 16 * rb + fr, 4 + g);
+        for (int rb = 0; rb < RBW; ++rb) {
+            fa[rb][0] = frag(buf, 16 * RBW * wv + 16 * rb + fr, g);
+            fa[rb][1] = frag(buf, 16 * RBW * wv + 16 * rb + fr, 4 + g);
         }
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
-            fw[cb][0] = frag(buf, TM + 16 * cb + fr, g);
-            fw[cb][1] = frag(buf, TM + 16 * cb + fr, 4 + g);
+            fw[cb][0] = frag(buf, TMR + 16 * cb + fr, g);
+            fw[cb][1] = frag(buf, TMR + 16 * cb + fr, 4 + g);
         }
         // transposed issue (W as the MFMA's A operand): a lane's 4 results are 4 consecutive
         // channels of one row -- one 16-byte store each.  Per accumulator: hh, hl, lh (X3).
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+        for (int rb = 0; rb < RBW; ++rb)
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb) {
                 if constexpr (X3) {
@@ -127,11 +131,11 @@ __global__ __launch_bounds__(256) void tail_split_kernel(ConvGemmParams p, int m
             __syncthreads();
         }
     }
-    // lane l of block (rb, cb): channels n0 + 16 cb + 4 g + 0..3 of row 64 wv + 16 rb + (l & 15)
+    // lane l of block (rb, cb): channels n0 + 16 cb + 4 g + 0..3 of row 16 RBW wv + 16 rb + (l & 15)
     float* const pbase = part + (size_t)slice * rows_pad * p.N;
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
-        const int mloc = mt0 + 64 * wv + 16 * rb + fr;
+    for (int rb = 0; rb < RBW; ++rb) {
+        const int mloc = mt0 + 16 * RBW * wv + 16 * rb + fr;
         if (m_begin + mloc >= p.M) continue;
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
@@ -342,15 +346,24 @@ hipError_t launch_conv_gemm_x3_shrink(const ConvGemmParams& p_in, hipStream_t st
     ConvGemmParams p = p_in;
     p.N = TN;
     const int chunk = (int)(kSplitPartBytes / ((size_t)S * TN * sizeof(float)) / TM * TM);
+    // below 32,768 rows 64-row workgroups (4x as many: 8,192 windows 0.026 ms vs 0.036 on the narrow
+    // exact-f32 kernel, profiles/r06_x3_small_shrink_ab.txt), the
+    // same per-output chains (bit-identical across batch sizes, test_config4_eight_shards_bit_equal)
+    const bool small = p_in.M < 32768;
     for (int m0 = 0; m0 < p_in.M; m0 += chunk) {
         const int m1 = m0 + chunk < p_in.M ? m0 + chunk : p_in.M;
         p.M = m1;  // the row bound of this chunk (rows past it clamp and are not stored)
         const int rows = m1 - m0;
-        const int mt = (rows + TM - 1) / TM;
-        hipLaunchKernelGGL((tail_split_kernel<f16, true>), dim3(1, S, mt), dim3(256), 0, stream, p, m0, mt * TM,
-                           (p.Kp / KS) / S, p.sk_part);
+        const int tmr = small ? 64 : TM;
+        const int mt = (rows + tmr - 1) / tmr;
+        if (small)
+            hipLaunchKernelGGL((tail_split_kernel<f16, true, 1>), dim3(1, S, mt), dim3(256), 0, stream, p, m0, mt * tmr,
+                               (p.Kp / KS) / S, p.sk_part);
+        else
+            hipLaunchKernelGGL((tail_split_kernel<f16, true, 4>), dim3(1, S, mt), dim3(256), 0, stream, p, m0, mt * tmr,
+                               (p.Kp / KS) / S, p.sk_part);
         const unsigned blocks = (unsigned)(((int64_t)rows * n_out + 255) / 256);
-        hipLaunchKernelGGL(shrink_reduce_x3_kernel, dim3(blocks), dim3(256), 0, stream, p, n_out, m0, rows, mt * TM, S,
+        hipLaunchKernelGGL(shrink_reduce_x3_kernel, dim3(blocks), dim3(256), 0, stream, p, n_out, m0, rows, mt * tmr, S,
                            (const float*)p.sk_part);
     }
     return hipGetLastError();
