@@ -50,7 +50,10 @@ def main():
         seq = [d]
         j = i + 1
         while j < len(ids) and len(seq) < len(LAYERS):
-            if "conv_gemm" in disp[ids[j]]["_name"]:
+            nm = disp[ids[j]]["_name"]
+            # (the f16x3 shrink since round 6: its split launch stands for the layer; config 4 at
+            # 65,536 windows has no other split-K tails)
+            if "conv_gemm" in nm or ("tail_split_kernel" in nm and len(seq) == len(LAYERS) - 1):
                 seq.append(disp[ids[j]])
             j += 1
         if len(seq) == len(LAYERS):
